@@ -1,0 +1,193 @@
+/*
+ * rtw.h — C-ABI of the MI355X-native render core (librtw_amd.so).
+ *
+ * Drop-in boundary for raytracer_weekend_lib's render hot path
+ * (reference: /root/reference, paths below relative to raytracer_weekend_lib/src/).
+ * The reference boundary is
+ *     Raytracer::new(world: &[Box<dyn Hittable>], cam: &Camera, background: Color,
+ *                    image_width: u32, image_height: u32, samples_per_pixel: u32)   lib.rs:40-48
+ *     Raytracer::render(&self) -> impl RenderIterator<Item = Pixel>                  lib.rs:57-76
+ * with the scene built through the Hittable/Material/Texture constructors listed per
+ * function below.  Because `dyn Hittable` has no introspection, the world crosses this
+ * boundary as a builder call stream (one call per reference constructor), is flattened
+ * once by rtw_scene_commit(), and rendered by rtw_render*().  INTEGRATION.md shows the
+ * Rust `extern "C"` block and the per-type `flatten` method a maintainer would add.
+ *
+ * Conventions: every int-returning function returns 0 on success or a negative
+ * errno-style code (RTW_E*), with a thread-local message in rtw_last_error().  The
+ * reference panics in the same situations (bvh.rs:57, material.rs:71, triangular.rs:178).
+ * Input arrays are copied; the caller keeps ownership.  A scene is immutable after
+ * rtw_scene_commit(); rendering is blocking on the given (or default) HIP stream.
+ * There is no CPU fallback: without a usable gfx950 device rtw_scene_commit() and the
+ * render calls fail with RTW_ENODEV.
+ */
+#ifndef RTW_H
+#define RTW_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTW_ABI_VERSION 1
+
+enum {
+  RTW_OK = 0,
+  RTW_EINVAL = -22,  /* bad argument (reference: panic / assert) */
+  RTW_ENOMEM = -12,
+  RTW_ENODEV = -19,  /* no HIP device / kernel launch failed */
+  RTW_ESTATE = -71,  /* call not valid in the scene's state (e.g. add after commit) */
+  RTW_EIO = -5       /* file / parse error (reference: unwrap on io / parse errors) */
+};
+
+typedef struct rtw_scene rtw_scene;
+
+/* camera.rs:9-20 Camera — filled by rtw_camera_new (camera.rs:25-64). */
+typedef struct {
+  float origin[3], lower_left_corner[3], horizontal[3], vertical[3];
+  float u[3], v[3], w[3];
+  float lens_radius, time0, time1;
+} rtw_camera;
+
+/* Render statistics. rays = number of world.hit queries (lib.rs:102). */
+typedef struct {
+  uint64_t rays;
+  uint64_t paths;          /* W*H*spp actually rendered */
+  double kernel_ms;        /* device time of the render kernel(s), HIP events */
+  double total_ms;         /* host wall time of the call (incl. D2H for rtw_render) */
+  uint64_t node_visits;    /* only when RTW_FLAG_COUNT_TRAVERSAL */
+  uint64_t prim_tests;     /* only when RTW_FLAG_COUNT_TRAVERSAL */
+  uint64_t prim_tests_by_type[6]; /* sphere, moving sphere, rect xy, xz, yz, triangle */
+} rtw_stats;
+
+enum { RTW_FLAG_COUNT_TRAVERSAL = 1 };
+
+const char* rtw_last_error(void);
+int rtw_abi_version(void);
+/* Number of visible HIP devices (0 in a GPU-less container; never initialises a context). */
+int rtw_device_count(void);
+
+/* ---- scene lifetime */
+int rtw_scene_create(rtw_scene** out);
+void rtw_scene_destroy(rtw_scene* scene);
+
+/* ---- textures: texture.rs:45-60 SolidColor::new/new_rgb, :62-81 Checker::new(odd, even, freq),
+ *      image_texture.rs:23-30 ImageTexture (decoded RGB8 pixels, row-major, top row first),
+ *      texture.rs:97-104 UVDebug */
+int rtw_texture_solid(rtw_scene* s, float r, float g, float b, uint32_t* id);
+int rtw_texture_checker(rtw_scene* s, uint32_t odd, uint32_t even, float frequency, uint32_t* id);
+int rtw_texture_image(rtw_scene* s, const uint8_t* rgb8, uint32_t width, uint32_t height, uint32_t* id);
+int rtw_texture_uvdebug(rtw_scene* s, uint32_t* id);
+
+/* ---- materials: material.rs:30-39 Lambertian::new, :63-73 Metal::new (fuzz <= 1 else
+ *      RTW_EINVAL, as the assert at :71), :102-105 Dielectric::new, light_source.rs:12-15
+ *      DiffuseLight::new */
+int rtw_material_lambertian(rtw_scene* s, uint32_t texture, uint32_t* id);
+int rtw_material_metal(rtw_scene* s, float r, float g, float b, float fuzz, uint32_t* id);
+int rtw_material_dielectric(rtw_scene* s, float index_of_refraction, uint32_t* id);
+int rtw_material_diffuse_light(rtw_scene* s, uint32_t texture, uint32_t* id);
+
+/* ---- hierarchy.  Objects are appended to the innermost open group (the world list at the
+ *      top).  Groups nest; each must be closed with rtw_end().
+ *      rtw_begin_list:      Vec<Box<dyn Hittable>>            hittable/mod.rs:57-69, 90-98
+ *      rtw_begin_bvh:       BvhNode::new(objects, t0, t1, rng)  bvh.rs:19-74
+ *      rtw_begin_translate: Translation::new(inner, offset)    transformations.rs:16-47
+ *      rtw_begin_rotate_y:  YRotation::new(inner, degrees)     transformations.rs:50-75
+ *      A wrapper applies to everything added inside it (= the wrapper of a list). */
+int rtw_begin_list(rtw_scene* s);
+int rtw_begin_bvh(rtw_scene* s, float time0, float time1);
+int rtw_begin_translate(rtw_scene* s, float x, float y, float z);
+int rtw_begin_rotate_y(rtw_scene* s, float degrees);
+int rtw_end(rtw_scene* s);
+
+/* ---- primitives (SoA arrays of length n; copied)
+ *      Sphere::new(center, radius, material)                spherical.rs:79-104
+ *      MovingSphere::new(c0, t0, c1, t1, radius, material)  spherical.rs:106-151
+ *      XY/XZ/YZRectangle::new(a0, a1, b0, b1, k, material)  rectangular.rs:16-166
+ *        axis: 0 = XY (k on z), 1 = XZ (k on y), 2 = YZ (k on x)
+ *      Cuboid::new(p0, p1, material)                        rectangular.rs:170-245
+ *      Triangle::new(vertices, [Option<normal>;3], [Option<uv>;3], material)  triangular.rs:33-73
+ *        verts: 9n floats; normals: 9n floats or NULL; normal_mask: n bytes (bit k = vertex k
+ *        has a normal) or NULL; uvs: 6n floats or NULL; uv_mask likewise. */
+int rtw_add_spheres(rtw_scene* s, uint32_t n, const float* cx, const float* cy, const float* cz,
+                    const float* radius, const uint32_t* material);
+int rtw_add_moving_spheres(rtw_scene* s, uint32_t n, const float* c0x, const float* c0y,
+                           const float* c0z, const float* t0, const float* c1x, const float* c1y,
+                           const float* c1z, const float* t1, const float* radius,
+                           const uint32_t* material);
+int rtw_add_rects(rtw_scene* s, uint32_t n, const uint32_t* axis, const float* a0, const float* a1,
+                  const float* b0, const float* b1, const float* k, const uint32_t* material);
+int rtw_add_cuboid(rtw_scene* s, const float p0[3], const float p1[3], uint32_t material);
+int rtw_add_triangles(rtw_scene* s, uint32_t n, const float* verts, const float* normals,
+                      const uint8_t* normal_mask, const float* uvs, const uint8_t* uv_mask,
+                      uint32_t material);
+
+/* load_wavefront_obj(path, rng) triangular.rs:241-260: adds BvhNode(triangles) to the open
+ * group.  Faces without a material get DiffuseLight(1,0,1) (:177-182); map_Kd images are
+ * decoded only if image_loader != NULL (the build ships no JPEG/PNG decoder; a missing
+ * loader or file is RTW_EIO as the reference's unwrap at :308).  `.rtwm` files (this
+ * build's binary mesh dump) are accepted too; their material is taken
+ * from `fallback_material` when != UINT32_MAX. */
+typedef int (*rtw_image_loader)(const char* path, uint8_t** rgb8, uint32_t* w, uint32_t* h);
+int rtw_load_wavefront_obj(rtw_scene* s, const char* path, rtw_image_loader image_loader,
+                           uint32_t fallback_material, uint32_t* n_triangles);
+
+/* Flatten the hierarchy, build the BVH and upload to every visible device (or only to
+ * `device` when >= 0).  After this the scene is immutable. */
+int rtw_scene_commit(rtw_scene* s, int device);
+
+/* Camera::new(look_from, look_at, vup, vfov, aspect, aperture, focus_dist, t0, t1) camera.rs:25-64 */
+int rtw_camera_new(const float look_from[3], const float look_at[3], const float vup[3],
+                   float vfov_degrees, float aspect_ratio, float aperture, float focus_dist,
+                   float time0, float time1, rtw_camera* out);
+
+/* Raytracer::new(world, cam, background, w, h, spp).render().collect() — lib.rs:40-95.
+ * out_rgb_sum (host, w*h*3 floats) receives the un-normalised Σ over spp per pixel in the
+ * reference's emission order (lib.rs:58: row j = h-1 .. 0, column i = 0 .. w-1), i.e.
+ * out[((h-1-j)*w + i)*3 + c].  max_depth is MAX_DEPTH (lib.rs:32, 50).  The per-sample
+ * random stream is keyed by (seed, j, i, sample) so the image is independent of tiling
+ * and device count. */
+int rtw_render(rtw_scene* s, const rtw_camera* cam, const float background[3], uint32_t w,
+               uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, float* out_rgb_sum,
+               rtw_stats* stats);
+
+/* Render a subset of 8x8 pixel tiles into device memory (multi-GPU / framework path).
+ * Tile t covers columns [8*tx, 8*tx+8) and output rows [8*ty, 8*ty+8) (row r <-> j = h-1-r),
+ * tile id = ty * ceil(w/8) + tx.  If d_tile_ids == NULL all tiles are rendered and d_out is a
+ * full w*h*3 image in reference order; otherwise d_tile_ids is a DEVICE array of n_tiles ids
+ * and d_out is packed [n_tiles][64][3] (pixels outside the image, and ids beyond the last tile,
+ * are left untouched).  `stream` is a hipStream_t (NULL = default).  The call only enqueues
+ * (graph-capturable) unless stats != NULL, in which case it synchronises and fills stats. */
+int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float background[3],
+                      uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
+                      const uint32_t* d_tile_ids, uint32_t n_tiles, float* d_out, void* stream,
+                      uint32_t flags, rtw_stats* stats);
+
+/* Scatter packed tiles (as written by rtw_render_device) into a full device image. */
+int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* d_tile_ids,
+                            uint32_t n_tiles, const float* d_packed, float* d_image, void* stream);
+
+/* console_app/src/main.rs:68-90 tonemap: sqrt(sum/spp), clamp [0, 0.999], u8(255.999*c). */
+int rtw_tonemap(const float* rgb_sum, uint32_t n_pixels, uint32_t spp, uint8_t* rgb8);
+
+/* ---- scene presets: console_app/src/scenes.rs restated (jumpy-balls :63-162,
+ *      cornell-box :350-414, wavefront-cow-obj :719-771, textured-monument :816-858,
+ *      two-spheres, simple-light, simple-triangle).  `seed` replaces thread_rng() for
+ *      the random placement; models_dir holds the meshes.  Fills cam and background. */
+int rtw_scene_preset(rtw_scene* s, const char* name, float aspect_ratio, uint64_t seed,
+                     const char* models_dir, rtw_camera* cam, float background[3]);
+
+/* Introspection for the test harness: the committed hierarchy as text (DESIGN.md
+ * §Scene text).  Returns the required size (incl. NUL) in *needed; writes when cap
+ * suffices.  rtw_scene_image(k) returns the k-th image texture's pixels. */
+int rtw_scene_dump(const rtw_scene* s, char* buf, size_t cap, size_t* needed);
+int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32_t* w, uint32_t* h);
+/* 0 leaf primitives, 1 materials, 2 textures, 3 BVH nodes, 4 BVH depth, 5 always-tested
+ * primitives, 6 instances */
+int64_t rtw_scene_info(const rtw_scene* s, int what);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,386 @@
+"""rtw_amd — Python host mirror of raytracer_weekend_lib's render API over the C-ABI.
+
+The product is ``lib/librtw_amd.so`` (HIP kernels for gfx950 + C++ host, include/rtw.h).
+This module is plumbing: ctypes bindings whose names and argument meaning follow the
+reference crate (raytracer_weekend_lib/src/), so tests read like the reference's API:
+
+    scene = Scene()
+    ground = scene.lambertian(scene.checker(scene.solid_rgb(.2, .3, .1), scene.solid_rgb(.9, .9, .9), 10))
+    scene.sphere((0, -1000, 0), 1000, ground)                  # Sphere::new        spherical.rs:79
+    with scene.translate((265, 0, 295)), scene.rotate_y(15):   # .rotate_y().translate()
+        scene.cuboid((0, 0, 0), (165, 330, 165), white)        # Cuboid::new        rectangular.rs:177
+    scene.commit()
+    cam = Camera.new((13, 2, 3), (0, 0, 0), (0, 1, 0), 20, 16 / 9, 0.1, 10, 0, 1)   # camera.rs:25
+    img, stats = Raytracer(scene, cam, (0.7, 0.8, 1.0), 400, 225, 50).render()       # lib.rs:40-76
+
+There is no CPU fallback: if the shared library is missing this module raises on load,
+and without a GPU ``Scene.commit`` raises ``RtwError(-19)``.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_ROOT = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "lib" / "librtw_amd.so"
+MODELS_DIR = REPO_ROOT / "models"
+
+RTW_EINVAL, RTW_ENOMEM, RTW_ENODEV, RTW_ESTATE, RTW_EIO = -22, -12, -19, -71, -5
+FLAG_COUNT_TRAVERSAL = 1
+NO_MATERIAL = 0xFFFFFFFF
+
+
+class RtwError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rtw error {code}: {msg}")
+        self.code = code
+
+
+class rtw_camera(C.Structure):  # include/rtw.h, camera.rs:9-20
+    _fields_ = [("origin", C.c_float * 3), ("lower_left_corner", C.c_float * 3),
+                ("horizontal", C.c_float * 3), ("vertical", C.c_float * 3),
+                ("u", C.c_float * 3), ("v", C.c_float * 3), ("w", C.c_float * 3),
+                ("lens_radius", C.c_float), ("time0", C.c_float), ("time1", C.c_float)]
+
+
+class rtw_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("kernel_ms", C.c_double),
+                ("total_ms", C.c_double), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("prim_tests_by_type", C.c_uint64 * 6)]
+
+    def as_dict(self) -> dict:
+        return {"rays": int(self.rays), "paths": int(self.paths), "kernel_ms": float(self.kernel_ms),
+                "total_ms": float(self.total_ms), "node_visits": int(self.node_visits),
+                "prim_tests": int(self.prim_tests),
+                "prim_tests_by_type": [int(x) for x in self.prim_tests_by_type]}
+
+
+_F = C.POINTER(C.c_float)
+_U32 = C.POINTER(C.c_uint32)
+_U8 = C.POINTER(C.c_uint8)
+_SIGS = {
+    "rtw_last_error": (C.c_char_p, []),
+    "rtw_abi_version": (C.c_int, []),
+    "rtw_device_count": (C.c_int, []),
+    "rtw_scene_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "rtw_scene_destroy": (None, [C.c_void_p]),
+    "rtw_texture_solid": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float, _U32]),
+    "rtw_texture_checker": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, _U32]),
+    "rtw_texture_image": (C.c_int, [C.c_void_p, _U8, C.c_uint32, C.c_uint32, _U32]),
+    "rtw_texture_uvdebug": (C.c_int, [C.c_void_p, _U32]),
+    "rtw_material_lambertian": (C.c_int, [C.c_void_p, C.c_uint32, _U32]),
+    "rtw_material_metal": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float, _U32]),
+    "rtw_material_dielectric": (C.c_int, [C.c_void_p, C.c_float, _U32]),
+    "rtw_material_diffuse_light": (C.c_int, [C.c_void_p, C.c_uint32, _U32]),
+    "rtw_begin_list": (C.c_int, [C.c_void_p]),
+    "rtw_begin_bvh": (C.c_int, [C.c_void_p, C.c_float, C.c_float]),
+    "rtw_begin_translate": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float]),
+    "rtw_begin_rotate_y": (C.c_int, [C.c_void_p, C.c_float]),
+    "rtw_end": (C.c_int, [C.c_void_p]),
+    "rtw_add_spheres": (C.c_int, [C.c_void_p, C.c_uint32, _F, _F, _F, _F, _U32]),
+    "rtw_add_moving_spheres": (C.c_int, [C.c_void_p, C.c_uint32] + [_F] * 9 + [_U32]),
+    "rtw_add_rects": (C.c_int, [C.c_void_p, C.c_uint32, _U32, _F, _F, _F, _F, _F, _U32]),
+    "rtw_add_cuboid": (C.c_int, [C.c_void_p, _F, _F, C.c_uint32]),
+    "rtw_add_triangles": (C.c_int, [C.c_void_p, C.c_uint32, _F, _F, _U8, _F, _U8, C.c_uint32]),
+    "rtw_load_wavefront_obj": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, _U32]),
+    "rtw_scene_commit": (C.c_int, [C.c_void_p, C.c_int]),
+    "rtw_camera_new": (C.c_int, [_F, _F, _F, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                                 C.c_float, C.POINTER(rtw_camera)]),
+    "rtw_render": (C.c_int, [C.c_void_p, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32, C.c_uint32,
+                             C.c_uint32, C.c_uint64, _F, C.POINTER(rtw_stats)]),
+    "rtw_render_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_uint32, C.c_uint64, _U32, C.c_uint32, C.c_void_p,
+                                    C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
+    "rtw_unpack_tiles_device": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
+    "rtw_scene_preset": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_uint64, C.c_char_p,
+                                   C.POINTER(rtw_camera), _F]),
+    "rtw_scene_dump": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rtw_scene_image": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(_U8), _U32, _U32]),
+    "rtw_scene_info": (C.c_int64, [C.c_void_p, C.c_int]),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load librtw_amd.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RtwError(RTW_ENODEV, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RtwError(rc, lib().rtw_last_error().decode())
+
+
+def _fa(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float32).reshape(-1))
+
+
+def _ua(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint32).reshape(-1))
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_F)
+
+
+def _up(a: np.ndarray):
+    return a.ctypes.data_as(_U32)
+
+
+def device_count() -> int:
+    return int(lib().rtw_device_count())
+
+
+class Camera:
+    """Camera::new (camera.rs:25-64)."""
+
+    def __init__(self, c: rtw_camera):
+        self.c = c
+
+    @classmethod
+    def new(cls, look_from, look_at, vup, vfov, aspect, aperture, focus_dist, time0=0.0, time1=1.0):
+        c = rtw_camera()
+        _check(lib().rtw_camera_new(_fp(_fa(look_from)), _fp(_fa(look_at)), _fp(_fa(vup)), vfov, aspect,
+                                    aperture, focus_dist, time0, time1, C.byref(c)))
+        return cls(c)
+
+    def as_dict(self) -> dict:
+        return {k: (list(getattr(self.c, k)) if k not in ("lens_radius", "time0", "time1")
+                    else float(getattr(self.c, k))) for k, _ in rtw_camera._fields_}
+
+
+class Scene:
+    """The world: Vec<Box<dyn Hittable>> plus its materials/textures, built by reference
+    constructor names (include/rtw.h documents the file:line each one replaces)."""
+
+    def __init__(self):
+        p = C.c_void_p()
+        _check(lib().rtw_scene_create(C.byref(p)))
+        self._p = p
+        self._keep = []
+
+    def __del__(self):
+        if getattr(self, "_p", None) and _lib is not None:
+            _lib.rtw_scene_destroy(self._p)
+            self._p = None
+
+    # textures ------------------------------------------------------------
+    def _id(self, fn, *args) -> int:
+        out = C.c_uint32()
+        _check(fn(self._p, *args, C.byref(out)))
+        return int(out.value)
+
+    def solid_rgb(self, r, g, b) -> int:
+        return self._id(lib().rtw_texture_solid, r, g, b)
+
+    def checker(self, odd: int, even: int, frequency: float) -> int:
+        return self._id(lib().rtw_texture_checker, odd, even, frequency)
+
+    def image(self, rgb8: np.ndarray) -> int:
+        a = np.ascontiguousarray(rgb8, dtype=np.uint8)
+        h, w, _ = a.shape
+        return self._id(lib().rtw_texture_image, a.ctypes.data_as(_U8), w, h)
+
+    def uv_debug(self) -> int:
+        return self._id(lib().rtw_texture_uvdebug)
+
+    # materials -----------------------------------------------------------
+    def lambertian(self, tex: int) -> int:
+        return self._id(lib().rtw_material_lambertian, tex)
+
+    def lambertian_solid(self, rgb) -> int:
+        return self.lambertian(self.solid_rgb(*rgb))
+
+    def metal(self, albedo, fuzz) -> int:
+        return self._id(lib().rtw_material_metal, albedo[0], albedo[1], albedo[2], fuzz)
+
+    def dielectric(self, ir) -> int:
+        return self._id(lib().rtw_material_dielectric, ir)
+
+    def diffuse_light(self, tex: int) -> int:
+        return self._id(lib().rtw_material_diffuse_light, tex)
+
+    # hierarchy -----------------------------------------------------------
+    @contextlib.contextmanager
+    def _group(self, rc):
+        _check(rc)
+        yield self
+        _check(lib().rtw_end(self._p))
+
+    def list(self):
+        return self._group(lib().rtw_begin_list(self._p))
+
+    def bvh(self, t0=0.0, t1=1.0):
+        return self._group(lib().rtw_begin_bvh(self._p, t0, t1))
+
+    def translate(self, offset):
+        return self._group(lib().rtw_begin_translate(self._p, *[float(x) for x in offset]))
+
+    def rotate_y(self, degrees):
+        return self._group(lib().rtw_begin_rotate_y(self._p, float(degrees)))
+
+    # primitives ----------------------------------------------------------
+    def spheres(self, centers, radii, mats) -> None:
+        c = np.asarray(centers, np.float32).reshape(-1, 3)
+        cx, cy, cz = (_fa(c[:, k]) for k in range(3))
+        r, m = _fa(radii), _ua(mats)
+        _check(lib().rtw_add_spheres(self._p, len(r), _fp(cx), _fp(cy), _fp(cz), _fp(r), _up(m)))
+
+    def sphere(self, center, radius, mat) -> None:
+        self.spheres([center], [radius], [mat])
+
+    def moving_spheres(self, c0, t0, c1, t1, radii, mats) -> None:
+        c0 = np.asarray(c0, np.float32).reshape(-1, 3)
+        c1 = np.asarray(c1, np.float32).reshape(-1, 3)
+        arrs = [_fa(c0[:, 0]), _fa(c0[:, 1]), _fa(c0[:, 2]), _fa(t0), _fa(c1[:, 0]), _fa(c1[:, 1]),
+                _fa(c1[:, 2]), _fa(t1), _fa(radii)]
+        m = _ua(mats)
+        _check(lib().rtw_add_moving_spheres(self._p, len(m), *[_fp(a) for a in arrs], _up(m)))
+
+    def moving_sphere(self, c0, t0, c1, t1, radius, mat) -> None:
+        self.moving_spheres([c0], [t0], [c1], [t1], [radius], [mat])
+
+    def rects(self, axis, a0, a1, b0, b1, k, mats) -> None:
+        ax = _ua(axis)
+        arrs = [_fa(a0), _fa(a1), _fa(b0), _fa(b1), _fa(k)]
+        m = _ua(mats)
+        _check(lib().rtw_add_rects(self._p, len(m), _up(ax), *[_fp(a) for a in arrs], _up(m)))
+
+    def xy_rect(self, x0, x1, y0, y1, k, mat):
+        self.rects([0], [x0], [x1], [y0], [y1], [k], [mat])
+
+    def xz_rect(self, x0, x1, z0, z1, k, mat):
+        self.rects([1], [x0], [x1], [z0], [z1], [k], [mat])
+
+    def yz_rect(self, y0, y1, z0, z1, k, mat):
+        self.rects([2], [y0], [y1], [z0], [z1], [k], [mat])
+
+    def cuboid(self, p0, p1, mat) -> None:
+        _check(lib().rtw_add_cuboid(self._p, _fp(_fa(p0)), _fp(_fa(p1)), mat))
+
+    def triangles(self, verts, mat, normals=None, normal_mask=None, uvs=None, uv_mask=None) -> None:
+        v = _fa(verts)
+        n = len(v) // 9
+        nn = _fa(normals) if normals is not None else None
+        uu = _fa(uvs) if uvs is not None else None
+        nm = np.ascontiguousarray(normal_mask, np.uint8) if normal_mask is not None else None
+        um = np.ascontiguousarray(uv_mask, np.uint8) if uv_mask is not None else None
+        _check(lib().rtw_add_triangles(
+            self._p, n, _fp(v), _fp(nn) if nn is not None else None,
+            nm.ctypes.data_as(_U8) if nm is not None else None, _fp(uu) if uu is not None else None,
+            um.ctypes.data_as(_U8) if um is not None else None, mat))
+
+    def load_wavefront_obj(self, path, material_override: int = NO_MATERIAL) -> int:
+        n = C.c_uint32()
+        _check(lib().rtw_load_wavefront_obj(self._p, str(path).encode(), None, material_override, C.byref(n)))
+        return int(n.value)
+
+    def preset(self, name: str, aspect: float, seed: int = 0, models_dir=None):
+        """console_app/src/scenes.rs scene by subcommand name -> (Camera, background)."""
+        cam = rtw_camera()
+        bg = np.zeros(3, np.float32)
+        md = str(models_dir or MODELS_DIR).encode()
+        _check(lib().rtw_scene_preset(self._p, name.encode(), aspect, seed, md, C.byref(cam), _fp(bg)))
+        return Camera(cam), tuple(float(x) for x in bg)
+
+    def commit(self, device: int = -1) -> "Scene":
+        _check(lib().rtw_scene_commit(self._p, device))
+        return self
+
+    # introspection -------------------------------------------------------
+    def dump(self) -> str:
+        need = C.c_size_t()
+        _check(lib().rtw_scene_dump(self._p, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        _check(lib().rtw_scene_dump(self._p, buf, need.value, C.byref(need)))
+        return buf.value.decode()
+
+    def images(self) -> list:
+        out, k = [], 0
+        while True:
+            px, w, h = _U8(), C.c_uint32(), C.c_uint32()
+            if lib().rtw_scene_image(self._p, k, C.byref(px), C.byref(w), C.byref(h)) != 0:
+                return out
+            out.append(np.ctypeslib.as_array(px, shape=(h.value * w.value * 3,)).copy())
+            k += 1
+
+    def info(self, what: int) -> int:
+        return int(lib().rtw_scene_info(self._p, what))
+
+
+class Raytracer:
+    """Raytracer::new(world, cam, background, w, h, spp) (lib.rs:40-48) + render() (:57-95)."""
+
+    def __init__(self, scene: Scene, cam: Camera, background, image_width: int, image_height: int,
+                 samples_per_pixel: int, seed: int = 0, max_depth: int = 50):
+        self.scene, self.cam = scene, cam
+        self.bg = _fa(background)
+        self.w, self.h, self.spp = int(image_width), int(image_height), int(samples_per_pixel)
+        self.seed, self.max_depth = int(seed), int(max_depth)
+
+    def render(self):
+        """-> (sums[h, w, 3] float32 in reference emission order: row r is j = h-1-r, stats)."""
+        out = np.empty((self.h, self.w, 3), np.float32)
+        st = rtw_stats()
+        _check(lib().rtw_render(self.scene._p, C.byref(self.cam.c), _fp(self.bg), self.w, self.h, self.spp,
+                                self.max_depth, self.seed, out.ctypes.data_as(_F), C.byref(st)))
+        return out, st.as_dict()
+
+    def render_device(self, d_out_ptr: int, device: int = 0, d_tiles_ptr: int = 0, n_tiles: int = 0,
+                      stream_ptr: int = 0, flags: int = 0, want_stats: bool = False):
+        """Enqueue into device memory.  d_tiles_ptr: device uint32 tile ids (0 = whole image,
+        full-layout output); with tiles the output is packed [n_tiles][64][3]."""
+        st = rtw_stats()
+        _check(lib().rtw_render_device(
+            self.scene._p, device, C.byref(self.cam.c), _fp(self.bg), self.w, self.h, self.spp, self.max_depth,
+            self.seed, C.cast(C.c_void_p(d_tiles_ptr), _U32) if d_tiles_ptr else None, n_tiles,
+            C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr), flags, C.byref(st) if want_stats else None))
+        return st.as_dict() if want_stats else None
+
+
+def unpack_tiles_device(w, h, d_tiles_ptr, n_tiles, d_packed_ptr, d_image_ptr, device=-1, stream_ptr=0):
+    _check(lib().rtw_unpack_tiles_device(device, w, h, C.c_void_p(d_tiles_ptr), n_tiles, C.c_void_p(d_packed_ptr),
+                                         C.c_void_p(d_image_ptr), C.c_void_p(stream_ptr)))
+
+
+def n_tiles(w: int, h: int) -> int:
+    return ((w + 7) // 8) * ((h + 7) // 8)
+
+
+def tonemap(sums: np.ndarray, spp: int) -> np.ndarray:
+    """console_app/src/main.rs:68-90 -> uint8 image of the same shape."""
+    s = np.ascontiguousarray(sums, np.float32)
+    out = np.empty(s.shape, np.uint8)
+    _check(lib().rtw_tonemap(_fp(s.reshape(-1)), s.size // 3, spp, out.ctypes.data_as(_U8)))
+    return out
+
+
+def image_height(width: int, aspect: float = 1.7777778) -> int:
+    """console_app/src/main.rs:33: (width as f64 / aspect).round() as u32 (ties away from zero)."""
+    import math
+    x = width / aspect
+    return int(math.floor(x + 0.5))
+
+
+def camera_aspect(width: int, height: int) -> float:
+    """console_app/src/main.rs:39: (w as f32) / (h as f32)."""
+    return float(np.float32(width) / np.float32(height))

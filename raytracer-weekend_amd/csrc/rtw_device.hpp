@@ -1,0 +1,108 @@
+// rtw_device.hpp — flattened scene layout in HBM, shared by the host flattener
+// (rtw_flatten.cpp) and the gfx950 kernels (rtw_kernel.hip).  Plain PODs only.
+//
+// Layout (DESIGN.md §Data layout):
+//   nodes   : DevNode[]   BVH2, 64 B per node = both children's boxes + child refs,
+//                         so one 64-B fetch (4 x dwordx4) tests two boxes.
+//   prims   : DevPrim[]   64 B per leaf primitive, stored in BVH leaf order so a leaf
+//                         is a contiguous run; geometry in q0..q2, meta in the last 16 B.
+//   always  : uint32[]    primitives tested for every ray (huge boxes, e.g. the
+//                         r=1000 ground sphere) instead of polluting the BVH.
+//   tshade  : DevTriShade per triangle: vertex normals + uvs, read only for the winner.
+//   insts   : DevInst[]   wrapper chains (Translation / YRotation), outer -> inner.
+//   mats, texs, texels   : material / texture tables and RGB8 image data.
+#pragma once
+#include <stdint.h>
+
+namespace rtw {
+
+enum PrimType : uint32_t {
+  PT_SPHERE = 0,
+  PT_MSPHERE = 1,
+  PT_RECT_XY = 2,
+  PT_RECT_XZ = 3,
+  PT_RECT_YZ = 4,
+  PT_TRI = 5,
+};
+
+struct alignas(16) DevPrim {
+  // sphere : q0 = (cx, cy, cz, r)
+  // msphere: q0 = (c0x, c0y, c0z, t0), q1 = (c1x, c1y, c1z, t1), q2.x = r
+  // rect   : q0 = (a0, a1, b0, b1), q1.x = k
+  // tri    : q0 = (ax, ay, az, abx), q1 = (aby, abz, acx, acy), q2 = (acz, nx, ny, nz)
+  //          ab = b - a, ac = c - a, n = ab x ac (bit-identical to triangular.rs:101-105)
+  float q0[4], q1[4], q2[4];
+  uint32_t type_inst;  // bits 0..7 PrimType, bits 8..31 instance id (0 = identity)
+  uint32_t key;        // global DFS leaf index: the tie-break (later object wins, mod.rs:61-65)
+  uint32_t mat;        // material id
+  uint32_t aux;        // triangle: index into tshade
+};
+static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
+
+struct alignas(16) DevNode {
+  float b0lo[3], b0hi[3];  // child 0 box
+  float b1lo[3], b1hi[3];  // child 1 box
+  int32_t c0, c1;          // child: node index (n == 0) or first prim (n > 0)
+  uint32_t n0, n1;         // prim count for leaf children, 0 for internal
+};
+static_assert(sizeof(DevNode) == 64, "DevNode must be 64 B");
+
+struct alignas(16) DevTriShade {
+  float n[9];   // vertex normals after defaults (triangular.rs:55)
+  float uv[6];  // vertex uvs after defaults (triangular.rs:57-66)
+  uint32_t pad;
+};
+static_assert(sizeof(DevTriShade) == 64, "DevTriShade must be 64 B");
+
+enum InstOp : uint32_t { IO_TRANSLATE = 1, IO_ROTY = 2 };
+constexpr int MAX_INST_OPS = 6;
+struct alignas(16) DevInst {
+  uint32_t nops, pad[3];
+  float op[MAX_INST_OPS][4];  // (type, x, y, z) translate  |  (type, sin, cos, 0) rotate_y
+};
+
+enum MatType : uint32_t { MT_LAMBERT = 0, MT_METAL = 1, MT_DIELECTRIC = 2, MT_LIGHT = 3 };
+struct alignas(16) DevMat {
+  uint32_t type, tex, needs_uv, pad;
+  float albedo[3];
+  float param;  // metal fuzz | dielectric ir
+};
+
+enum TexType : uint32_t { TT_SOLID = 0, TT_CHECKER = 1, TT_IMAGE = 2, TT_UVDEBUG = 3 };
+struct alignas(16) DevTex {
+  uint32_t type, odd, even, pad;
+  float c[3], freq;
+  uint32_t off, w, h, pad2;  // texels[off .. off + 3*w*h)
+};
+
+struct DevScene {
+  const DevNode* nodes;
+  const DevPrim* prims;
+  const uint32_t* always;
+  const DevTriShade* tshade;
+  const DevInst* insts;
+  const DevMat* mats;
+  const DevTex* texs;
+  const uint8_t* texels;
+  uint32_t n_nodes, n_prims, n_always, n_insts;
+};
+
+struct DevCamera {
+  float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
+  float lens_radius, time0, time1;
+};
+
+struct RenderArgs {
+  DevScene scene;
+  DevCamera cam;
+  float bg[3];
+  uint32_t w, h, spp, max_depth;
+  uint32_t tiles_x;           // ceil(w / 8)
+  uint32_t n_tiles;           // tiles to render
+  const uint32_t* tile_ids;   // device array or nullptr (= tiles 0..n_tiles-1, full-image output)
+  uint64_t seed_hash;         // splitmix64(seed)
+  float* out;
+  unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
+};
+
+}  // namespace rtw

@@ -1,0 +1,430 @@
+// rtw_flatten.cpp — turns the reference-shaped Hittable tree into the device layout
+// (rtw_device.hpp): one BVH2 over every leaf primitive in world space, each primitive
+// tagged with its wrapper chain (instance) and its DFS key.
+//
+// Why this is exact w.r.t. the reference's nested closest-hit (hittable/mod.rs:57-69):
+// every reference set (Vec list, Cuboid sides, BvhNode) returns the closest hit of its
+// children and a later child wins an exact tie, and t is the same number in every
+// wrapper space (Translation/YRotation do not rescale the ray).  So the world's answer is
+// "smallest candidate t over all leaves, ties to the largest DFS key", which is a
+// commutative reduction any traversal order reproduces, provided culling never drops a
+// leaf whose candidate could win.  Culling is made conservative by padding every box
+// (pad_box) and by a relative slack on the best t in the kernel.  Primitives whose box
+// is huge next to the rest (the r = 1000 ground sphere, scenes.rs:74-78) are kept out of
+// the BVH and tested for every ray ("always" list): it keeps the tree tight and removes
+// the grazing-ray precision cases of a 1000-unit sphere from the culling argument.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <vector>
+
+#include "../../include/rtw.h"
+#include "rtw_scene.hpp"
+
+namespace rtw {
+namespace {
+
+struct Box {
+  float lo[3] = {INFINITY, INFINITY, INFINITY};
+  float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const float p[3]) {
+    for (int a = 0; a < 3; ++a) { lo[a] = fminf(lo[a], p[a]); hi[a] = fmaxf(hi[a], p[a]); }
+  }
+  void grow(const Box& b) {
+    for (int a = 0; a < 3; ++a) { lo[a] = fminf(lo[a], b.lo[a]); hi[a] = fmaxf(hi[a], b.hi[a]); }
+  }
+  bool valid() const { return lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2]; }
+  float area() const {
+    if (!valid()) return 0.f;
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.f * (dx * dy + dy * dz + dz * dx);
+  }
+  float diag() const {
+    if (!valid()) return 0.f;
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return sqrtf(dx * dx + dy * dy + dz * dz);
+  }
+};
+
+// Conservative padding: covers the rounding of the primitive tests and of the slab test
+// (errors scale with coordinate magnitude, ~1e-6 relative for well-conditioned hits).
+void pad_box(Box& b) {
+  float m = 0.f;
+  for (int a = 0; a < 3; ++a) m = fmaxf(m, fmaxf(fabsf(b.lo[a]), fabsf(b.hi[a])));
+  float e = 1e-4f + 4e-5f * m;
+  for (int a = 0; a < 3; ++a) { b.lo[a] -= e; b.hi[a] += e; }
+}
+
+struct Leaf {
+  DevPrim p;
+  Box wbox;
+  float c[3];
+};
+
+struct Builder {
+  const Scene& s;
+  Flat& f;
+  std::map<std::vector<uint32_t>, uint32_t> inst_of;
+  std::vector<Leaf> leaves;
+  uint32_t key = 0;
+  int err = RTW_OK;
+
+  Builder(const Scene& sc, Flat& fl) : s(sc), f(fl) {}
+
+  uint32_t instance(const std::vector<uint32_t>& chain) {
+    if (chain.empty()) return 0;
+    auto it = inst_of.find(chain);
+    if (it != inst_of.end()) return it->second;
+    if (chain.size() > (size_t)MAX_INST_OPS) {
+      err = fail(RTW_EINVAL, "wrapper chain deeper than %d", MAX_INST_OPS);
+      return 0;
+    }
+    DevInst in;
+    memset(&in, 0, sizeof in);
+    in.nops = (uint32_t)chain.size();
+    for (size_t k = 0; k < chain.size(); ++k) {
+      const Node& n = s.nodes[chain[k]];
+      if (n.kind == NK_TRANSLATE) {
+        in.op[k][0] = (float)IO_TRANSLATE;
+        in.op[k][1] = n.f[0]; in.op[k][2] = n.f[1]; in.op[k][3] = n.f[2];
+      } else {
+        in.op[k][0] = (float)IO_ROTY;
+        in.op[k][1] = n.sin_t; in.op[k][2] = n.cos_t;
+      }
+    }
+    uint32_t id = (uint32_t)f.insts.size();
+    f.insts.push_back(in);
+    inst_of[chain] = id;
+    return id;
+  }
+
+  // object-space box -> world box through the wrapper chain (inner -> outer)
+  Box to_world(Box b, const std::vector<uint32_t>& chain) {
+    pad_box(b);
+    for (size_t k = chain.size(); k-- > 0;) {
+      const Node& n = s.nodes[chain[k]];
+      if (n.kind == NK_TRANSLATE) {
+        for (int a = 0; a < 3; ++a) { b.lo[a] += n.f[a]; b.hi[a] += n.f[a]; }
+      } else {  // object -> world of YRotation::hit (transformations.rs:137-141)
+        Box r;
+        for (int q = 0; q < 8; ++q) {
+          float x = (q & 1) ? b.hi[0] : b.lo[0], y = (q & 2) ? b.hi[1] : b.lo[1], z = (q & 4) ? b.hi[2] : b.lo[2];
+          float p[3] = {n.cos_t * x + n.sin_t * z, y, -n.sin_t * x + n.cos_t * z};
+          r.grow(p);
+        }
+        b = r;
+      }
+      pad_box(b);
+    }
+    return b;
+  }
+
+  void emit(DevPrim p, Box local, const std::vector<uint32_t>& chain) {
+    p.type_inst |= instance(chain) << 8;
+    p.key = key++;
+    Leaf L;
+    L.p = p;
+    L.wbox = to_world(local, chain);
+    for (int a = 0; a < 3; ++a) L.c[a] = 0.5f * (L.wbox.lo[a] + L.wbox.hi[a]);
+    leaves.push_back(L);
+  }
+
+  void rect(uint32_t axis, float a0, float a1, float b0, float b1, float k, uint32_t mat,
+            const std::vector<uint32_t>& chain) {
+    DevPrim p;
+    memset(&p, 0, sizeof p);
+    p.type_inst = PT_RECT_XY + axis;
+    p.q0[0] = a0; p.q0[1] = a1; p.q0[2] = b0; p.q0[3] = b1; p.q1[0] = k;
+    p.mat = mat;
+    Box b;
+    float lo[3], hi[3];
+    int kax = axis == 0 ? 2 : (axis == 1 ? 1 : 0), aax = axis == 2 ? 1 : 0, bax = axis == 0 ? 1 : 2;
+    lo[aax] = fminf(a0, a1); hi[aax] = fmaxf(a0, a1);
+    lo[bax] = fminf(b0, b1); hi[bax] = fmaxf(b0, b1);
+    lo[kax] = k; hi[kax] = k;
+    b.grow(lo); b.grow(hi);
+    emit(p, b, chain);
+  }
+
+  void walk(uint32_t id, std::vector<uint32_t>& chain) {
+    const Node& n = s.nodes[id];
+    switch (n.kind) {
+      case NK_LIST:
+      case NK_BVH:
+        for (uint32_t c : n.ch) walk(c, chain);
+        return;
+      case NK_TRANSLATE:
+      case NK_ROTY:
+        chain.push_back(id);
+        for (uint32_t c : n.ch) walk(c, chain);
+        chain.pop_back();
+        return;
+      case NK_SPHERE: {
+        DevPrim p;
+        memset(&p, 0, sizeof p);
+        p.type_inst = PT_SPHERE;
+        memcpy(p.q0, n.f, 4 * sizeof(float));
+        p.mat = n.mat;
+        float r = fabsf(n.f[3]);  // |r|: spherical.rs:98-103 inverts the box for r < 0
+        Box b;
+        float lo[3] = {n.f[0] - r, n.f[1] - r, n.f[2] - r}, hi[3] = {n.f[0] + r, n.f[1] + r, n.f[2] + r};
+        b.grow(lo); b.grow(hi);
+        emit(p, b, chain);
+        return;
+      }
+      case NK_MSPHERE: {
+        DevPrim p;
+        memset(&p, 0, sizeof p);
+        p.type_inst = PT_MSPHERE;
+        memcpy(p.q0, n.f, 4 * sizeof(float));
+        memcpy(p.q1, n.f + 4, 4 * sizeof(float));
+        p.q2[0] = n.f[8];
+        p.mat = n.mat;
+        float r = fabsf(n.f[8]);
+        Box b;
+        // center_at_time (spherical.rs:117-123) is linear in t: the shutter interval's end
+        // points bound it.  The kernel refuses cameras outside [time_lo, time_hi].
+        for (float t : {f.time_lo, f.time_hi}) {
+          float c[3];
+          for (int a = 0; a < 3; ++a) c[a] = n.f[a] + ((t - n.f[3]) / (n.f[7] - n.f[3])) * (n.f[4 + a] - n.f[a]);
+          float lo[3] = {c[0] - r, c[1] - r, c[2] - r}, hi[3] = {c[0] + r, c[1] + r, c[2] + r};
+          b.grow(lo); b.grow(hi);
+        }
+        emit(p, b, chain);
+        return;
+      }
+      case NK_RECT:
+        rect(n.axis, n.f[0], n.f[1], n.f[2], n.f[3], n.f[4], n.mat, chain);
+        return;
+      case NK_CUBOID: {  // rectangular.rs:177-234, sides in this order
+        const float* p0 = n.f;
+        const float* p1 = n.f + 3;
+        rect(0, p0[0], p1[0], p0[1], p1[1], p1[2], n.mat, chain);
+        rect(0, p0[0], p1[0], p0[1], p1[1], p0[2], n.mat, chain);
+        rect(1, p0[0], p1[0], p0[2], p1[2], p1[1], n.mat, chain);
+        rect(1, p0[0], p1[0], p0[2], p1[2], p0[1], n.mat, chain);
+        rect(2, p0[1], p1[1], p0[2], p1[2], p1[0], n.mat, chain);
+        rect(2, p0[1], p1[1], p0[2], p1[2], p0[0], n.mat, chain);
+        return;
+      }
+      case NK_TRI: {
+        const float* v = &s.tri_v[9 * (size_t)n.tri];
+        DevPrim p;
+        memset(&p, 0, sizeof p);
+        p.type_inst = PT_TRI;
+        // triangular.rs:101-105: ab = b - a, ac = c - a, n = ab x ac (precomputed, bit-identical)
+        float ab[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+        float ac[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        float nn[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2], ab[0] * ac[1] - ab[1] * ac[0]};
+        float q[12] = {v[0], v[1], v[2], ab[0], ab[1], ab[2], ac[0], ac[1], ac[2], nn[0], nn[1], nn[2]};
+        memcpy(p.q0, q, 4 * sizeof(float));
+        memcpy(p.q1, q + 4, 4 * sizeof(float));
+        memcpy(p.q2, q + 8, 4 * sizeof(float));
+        p.mat = n.mat;
+        p.aux = (uint32_t)f.tshade.size();
+        DevTriShade sh;
+        memset(&sh, 0, sizeof sh);
+        const float* vn = &s.tri_n[9 * (size_t)n.tri];
+        const float* uv = &s.tri_uv[6 * (size_t)n.tri];
+        const float defuv[6] = {0, 0, 1, 0, 0, 1};  // triangular.rs:57-61
+        uint8_t nm = s.tri_nm[n.tri], um = s.tri_uvm[n.tri];
+        for (int k = 0; k < 3; ++k) {
+          for (int a = 0; a < 3; ++a) sh.n[3 * k + a] = ((nm >> k) & 1) ? vn[3 * k + a] : nn[a];  // :55
+          for (int a = 0; a < 2; ++a) sh.uv[2 * k + a] = ((um >> k) & 1) ? uv[2 * k + a] : defuv[2 * k + a];
+        }
+        f.tshade.push_back(sh);
+        Box b;
+        for (int k = 0; k < 3; ++k) b.grow(v + 3 * k);
+        emit(p, b, chain);
+        return;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------- binned SAH BVH2
+constexpr int LEAF_MAX = 4;
+constexpr int NBINS = 16;
+constexpr uint32_t MAX_DEPTH = 31;  // the kernel's traversal stack holds 32 entries
+
+struct Ref {
+  Box box;
+  int32_t idx;     // node index (count == 0) or first prim
+  uint32_t count;  // prims in leaf
+};
+
+struct BvhBuild {
+  std::vector<Leaf>& L;
+  std::vector<DevNode>& nodes;
+  uint32_t median_depth;  // from here on: median splits, so depth <= MAX_DEPTH
+  uint32_t max_depth = 0;
+
+  Ref build(uint32_t b, uint32_t e, uint32_t depth) {
+    Box box, cbox;
+    for (uint32_t k = b; k < e; ++k) { box.grow(L[k].wbox); cbox.grow(L[k].c); }
+    uint32_t n = e - b;
+    if (depth > max_depth) max_depth = depth;
+    if (n <= 2) return Ref{box, (int32_t)b, n};
+
+    // choose split
+    int best_axis = -1;
+    int best_bin = 0;
+    float best_cost = INFINITY;
+    if (depth < median_depth) {
+      for (int a = 0; a < 3; ++a) {
+        float lo = cbox.lo[a], hi = cbox.hi[a];
+        if (!(hi > lo)) continue;
+        Box bb[NBINS];
+        uint32_t cnt[NBINS] = {0};
+        float sc = NBINS / (hi - lo);
+        for (uint32_t k = b; k < e; ++k) {
+          int bi = std::min(NBINS - 1, (int)((L[k].c[a] - lo) * sc));
+          cnt[bi]++;
+          bb[bi].grow(L[k].wbox);
+        }
+        Box left[NBINS];
+        uint32_t lc[NBINS];
+        Box acc;
+        uint32_t c = 0;
+        for (int q = 0; q < NBINS; ++q) { acc.grow(bb[q]); c += cnt[q]; left[q] = acc; lc[q] = c; }
+        acc = Box();
+        c = 0;
+        for (int q = NBINS - 1; q > 0; --q) {
+          acc.grow(bb[q]);
+          c += cnt[q];
+          if (lc[q - 1] == 0 || c == 0) continue;
+          float cost = left[q - 1].area() * lc[q - 1] + acc.area() * c;
+          if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = q; }
+        }
+      }
+      float leaf_cost = box.area() * n;
+      float split_cost = box.area() * 0.5f + best_cost;  // traversal ~ half a prim test
+      if (n <= LEAF_MAX && (best_axis < 0 || split_cost >= leaf_cost))
+        return Ref{box, (int32_t)b, n};
+    }
+    uint32_t mid;
+    if (best_axis >= 0) {
+      float lo = cbox.lo[best_axis], sc = NBINS / (cbox.hi[best_axis] - lo);
+      auto it = std::partition(L.begin() + b, L.begin() + e, [&](const Leaf& x) {
+        return std::min(NBINS - 1, (int)((x.c[best_axis] - lo) * sc)) < best_bin;
+      });
+      mid = (uint32_t)(it - L.begin());
+      if (mid == b || mid == e) best_axis = -1;
+    }
+    if (best_axis < 0) {  // median split on the widest centroid axis
+      int a = 0;
+      for (int q = 1; q < 3; ++q)
+        if (cbox.hi[q] - cbox.lo[q] > cbox.hi[a] - cbox.lo[a]) a = q;
+      mid = b + n / 2;
+      std::nth_element(L.begin() + b, L.begin() + mid, L.begin() + e,
+                       [a](const Leaf& x, const Leaf& y) { return x.c[a] < y.c[a]; });
+    }
+    int32_t id = (int32_t)nodes.size();
+    nodes.push_back(DevNode{});
+    Ref l = build(b, mid, depth + 1);
+    Ref r = build(mid, e, depth + 1);
+    DevNode& nd = nodes[id];
+    for (int a = 0; a < 3; ++a) {
+      nd.b0lo[a] = l.box.lo[a]; nd.b0hi[a] = l.box.hi[a];
+      nd.b1lo[a] = r.box.lo[a]; nd.b1hi[a] = r.box.hi[a];
+    }
+    nd.c0 = l.idx; nd.n0 = l.count;
+    nd.c1 = r.idx; nd.n1 = r.count;
+    return Ref{box, id, 0};
+  }
+};
+
+bool texture_reads_uv(const Scene& s, uint32_t t, int guard = 0) {
+  if (guard > 64) return false;
+  const TexH& x = s.tex[t];
+  if (x.type == TT_IMAGE || x.type == TT_UVDEBUG) return true;
+  if (x.type == TT_CHECKER) return texture_reads_uv(s, x.odd, guard + 1) || texture_reads_uv(s, x.even, guard + 1);
+  return false;
+}
+
+}  // namespace
+
+int flatten(Scene& s) {
+  Flat& f = s.flat;
+  f = Flat();
+  // tables
+  for (const MatH& m : s.mat) {
+    DevMat d;
+    memset(&d, 0, sizeof d);
+    d.type = m.type; d.tex = m.tex; d.param = m.param;
+    memcpy(d.albedo, m.albedo, sizeof d.albedo);
+    d.needs_uv = (m.type == MT_LAMBERT || m.type == MT_LIGHT) ? texture_reads_uv(s, m.tex) : 0;
+    f.mats.push_back(d);
+  }
+  for (const TexH& t : s.tex) {
+    DevTex d;
+    memset(&d, 0, sizeof d);
+    d.type = t.type; d.odd = t.odd; d.even = t.even; d.freq = t.freq;
+    memcpy(d.c, t.c, sizeof d.c);
+    if (t.type == TT_IMAGE) {
+      d.off = (uint32_t)f.texels.size();
+      d.w = t.w; d.h = t.h;
+      f.texels.insert(f.texels.end(), t.img.begin(), t.img.end());
+    }
+    f.texs.push_back(d);
+  }
+  if (f.texels.empty()) f.texels.resize(4, 0);
+  if (f.mats.empty()) f.mats.push_back(DevMat{});
+  if (f.texs.empty()) f.texs.push_back(DevTex{});
+
+  DevInst ident;
+  memset(&ident, 0, sizeof ident);
+  f.insts.push_back(ident);
+
+  Builder B(s, f);
+  std::vector<uint32_t> chain;
+  B.walk(0, chain);
+  if (B.err) return B.err;
+  if (B.leaves.size() >= (1u << 31)) return fail(RTW_EINVAL, "too many primitives");
+
+  // split off huge primitives (tested for every ray)
+  std::vector<Leaf> huge, rest;
+  if (B.leaves.size() > 16) {
+    std::vector<float> d;
+    for (const Leaf& L : B.leaves) d.push_back(L.wbox.diag());
+    std::vector<float> sorted = d;
+    size_t q = (size_t)(0.95 * (sorted.size() - 1));
+    std::nth_element(sorted.begin(), sorted.begin() + q, sorted.end());
+    float thr = 20.f * sorted[q];
+    size_t nh = 0;
+    for (float x : d) nh += x > thr;
+    for (size_t k = 0; k < B.leaves.size(); ++k)
+      ((nh <= 8 && d[k] > thr) ? huge : rest).push_back(B.leaves[k]);
+  } else {
+    rest = B.leaves;
+  }
+
+  if (!rest.empty()) {
+    uint32_t lg = 0;
+    while ((1ull << lg) < rest.size()) ++lg;
+    BvhBuild bb{rest, f.nodes, lg + 4 < MAX_DEPTH ? MAX_DEPTH - lg - 1 : 3};
+    Ref root = bb.build(0, (uint32_t)rest.size(), 0);
+    if (root.count > 0) {  // whole set is one leaf: wrap it in a root node
+      DevNode nd;
+      for (int a = 0; a < 3; ++a) {
+        nd.b0lo[a] = root.box.lo[a]; nd.b0hi[a] = root.box.hi[a];
+        nd.b1lo[a] = INFINITY; nd.b1hi[a] = -INFINITY;
+      }
+      nd.c0 = root.idx; nd.n0 = root.count;
+      nd.c1 = 0; nd.n1 = 0;
+      f.nodes.push_back(nd);
+    }
+    f.depth = bb.max_depth;
+  }
+  for (const Leaf& L : rest) f.prims.push_back(L.p);
+  for (const Leaf& L : huge) {
+    f.always.push_back((uint32_t)f.prims.size());
+    f.prims.push_back(L.p);
+  }
+  if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  return RTW_OK;
+}
+
+}  // namespace rtw

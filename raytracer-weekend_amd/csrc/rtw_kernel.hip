@@ -1,0 +1,744 @@
+// rtw_kernel.hip — gfx950 path-tracing megakernel and the device half of the C-ABI.
+//
+// Hot path restated (reference raytracer_weekend_lib/src/):
+//   Raytracer::render / sample_pixel (lib.rs:57-95)   -> one lane per pixel, samples in order
+//   sample_ray (lib.rs:97-117)                          -> iterative bounce loop, L = T * terminal
+//   [Box<dyn Hittable>]::hit (hittable/mod.rs:57-69)    -> BVH2 traversal, min t, ties -> max key
+//   Material::scatter / emitted (material.rs, light_source.rs), Texture::value (texture.rs,
+//   image_texture.rs), Camera::get_ray (camera.rs:66-74)
+//
+// Numerics: compiled with -ffp-contract=off and IEEE div/sqrt (hipcc's default
+// -fhip-fp32-correctly-rounded-divide-sqrt), so every primitive test, scatter and the
+// throughput product are bit-identical to the oracle's iterative integrator.  Only the
+// BVH culling uses FMA / rcp, and it is conservative (padded boxes + slack), so it
+// changes which nodes are visited, never the answer.
+//
+// Wave structure: a workgroup is 4 waves; each wave owns one 8x8 pixel tile (coherent
+// camera rays).  A lane loops over its pixel's samples with path regeneration: every
+// loop iteration traces exactly one segment, and a lane whose path ended starts its
+// next sample in the same iteration, so lanes stay busy across paths of 1..50 bounces.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <chrono>
+
+#include "../../include/rtw.h"
+#include "rtw_scene.hpp"
+
+namespace rtw {
+namespace dev {
+
+constexpr float TMIN = 0.001f;  // lib.rs:102
+constexpr int BLOCK = 256;
+constexpr int STACK = 32;
+
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 scale(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 divs(V3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ V3 unit(V3 a) { return divs(a, sqrtf(len2(a))); }       // vec3.rs:85-87
+__device__ __forceinline__ bool near_zero(V3 a) {                                   // vec3.rs:133-138
+  return fabsf(a.x) < 1e-8f && fabsf(a.y) < 1e-8f && fabsf(a.z) < 1e-8f;
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }  // :140-142
+__device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                                  // :144-151
+  float cos_t = fminf(dot(neg(uv), n), 1.0f);
+  V3 perp = scale(add(uv, scale(n, cos_t)), eta);
+  float k = -sqrtf(fabsf(1.0f - len2(perp)));
+  return add(perp, scale(n, k));
+}
+__device__ __forceinline__ V3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+// ---- RNG: PCG32 XSH-RR keyed by (seed, pixel, sample); rand 0.9 float conversions
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
+  uint64_t old = s;
+  s = old * 6364136223846793005ull + 1442695040888963407ull;
+  uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+  uint32_t rot = (uint32_t)(old >> 59);
+  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+__device__ __forceinline__ float gen_f32(uint64_t& s) {  // rand Standard<f32>
+  return (float)(pcg_next(s) >> 8) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi) {  // UniformFloat::sample_single
+  float sc = hi - lo;
+  for (;;) {
+    float v01 = __uint_as_float((pcg_next(s) >> 9) | 0x3F800000u) - 1.0f;
+    float r = v01 * sc + lo;
+    if (r < hi) return r;
+    sc = __uint_as_float(__float_as_uint(sc) - 1u);
+  }
+}
+__device__ __forceinline__ V3 rand_in_unit_sphere(uint64_t& s) {  // vec3.rs:101-108
+  for (;;) {
+    float x = gen_range(s, -1.0f, 1.0f);
+    float y = gen_range(s, -1.0f, 1.0f);
+    float z = gen_range(s, -1.0f, 1.0f);
+    V3 p = mk(x, y, z);
+    if (len2(p) < 1.0f) return p;
+  }
+}
+__device__ __forceinline__ V3 rand_in_unit_disk(uint64_t& s) {  // vec3.rs:124-131
+  for (;;) {
+    float x = gen_range(s, -1.0f, 1.0f);
+    float y = gen_range(s, -1.0f, 1.0f);
+    V3 p = mk(x, y, 0.0f);
+    if (len2(p) < 1.0f) return p;
+  }
+}
+
+struct Ray { V3 o, d; float time; };
+
+// ---- wrapper chains (transformations.rs:23-38, :115-135): world ray -> object ray
+__device__ __forceinline__ Ray to_local(const DevInst* in, Ray r) {
+  const uint32_t n = in->nops;
+  for (uint32_t k = 0; k < n; ++k) {
+    const float4 op = *reinterpret_cast<const float4*>(in->op[k]);
+    if (op.x == (float)IO_TRANSLATE) {
+      r.o = sub(r.o, mk(op.y, op.z, op.w));
+    } else {
+      const float s = op.y, c = op.z;
+      r.o = mk(c * r.o.x - s * r.o.z, r.o.y, s * r.o.x + c * r.o.z);
+      r.d = mk(c * r.d.x - s * r.d.z, r.d.y, s * r.d.x + c * r.d.z);
+    }
+  }
+  return r;
+}
+
+// ---- candidate t of one primitive (independent of t_max; -1 = miss)
+__device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad) {  // spherical.rs:26-44
+  V3 oc = sub(r.o, c);
+  float a = len2(r.d);
+  float hb = dot(oc, r.d);
+  float cc = len2(oc) - rad * rad;
+  float disc = hb * hb - a * cc;
+  if (!(disc >= 0.0f)) return -1.0f;
+  float sq = sqrtf(disc);
+  float root = (-hb - sq) / a;
+  if (root < TMIN) root = (-hb + sq) / a;  // root1 > t_max implies root2 > t_max
+  return root;
+}
+__device__ __forceinline__ V3 center_at(const float* q0, const float* q1, float time) {  // :117-123
+  V3 c0 = ld3(q0), c1 = ld3(q1);
+  return add(c0, scale(sub(c1, c0), (time - q0[3]) / (q1[3] - q0[3])));
+}
+template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
+__device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float k) {
+  const float o_k = AXIS == 0 ? r.o.z : (AXIS == 1 ? r.o.y : r.o.x);
+  const float d_k = AXIS == 0 ? r.d.z : (AXIS == 1 ? r.d.y : r.d.x);
+  const float o_a = AXIS == 2 ? r.o.y : r.o.x, d_a = AXIS == 2 ? r.d.y : r.d.x;
+  const float o_b = AXIS == 0 ? r.o.y : r.o.z, d_b = AXIS == 0 ? r.d.y : r.d.z;
+  float t = (k - o_k) / d_k;
+  if (t < TMIN) return -1.0f;
+  float x = o_a + t * d_a;
+  float y = o_b + t * d_b;
+  if (x < q0[0] || x > q0[1] || y < q0[2] || y > q0[3]) return -1.0f;
+  return t;
+}
+struct TriUV { float t, u, v; };
+__device__ __forceinline__ TriUV tri_solve(const Ray& r, const float* q) {  // triangular.rs:98-118
+  V3 a = mk(q[0], q[1], q[2]), ab = mk(q[3], q[4], q[5]), ac = mk(q[6], q[7], q[8]);
+  V3 n = mk(q[9], q[10], q[11]);
+  float det = -dot(r.d, n);
+  float inv = 1.0f / det;
+  V3 ao = sub(r.o, a);
+  V3 aoxd = cross(ao, r.d);
+  TriUV o;
+  o.u = dot(ac, aoxd) * inv;
+  o.v = -dot(ab, aoxd) * inv;
+  o.t = dot(ao, n) * inv;
+  return o;
+}
+__device__ __forceinline__ float cand_tri(const Ray& r, const float* q) {
+  TriUV s = tri_solve(r, q);
+  if (s.t < TMIN) return -1.0f;
+  if (!(s.t >= 0.0f && s.u >= 0.0f && s.v >= 0.0f && (s.u + s.v) <= 1.0f)) return -1.0f;
+  return s.t;
+}
+
+struct Best { float t; uint32_t key; int32_t prim; };
+
+template <bool COUNT>
+__device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr,
+                                          uint32_t& cur_inst, Ray& lr, Best& b, uint32_t* cnt) {
+  const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
+  const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
+  const float4 q0v = P[0];
+  const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
+  if (inst != cur_inst) {
+    cur_inst = inst;
+    lr = inst ? to_local(S.insts + inst, wr) : wr;
+  }
+  float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
+  float t;
+  if (type == PT_SPHERE) {
+    t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3]);
+  } else if (type == PT_MSPHERE) {
+    const float4 q1v = P[1];
+    const float q1[4] = {q1v.x, q1v.y, q1v.z, q1v.w};
+    const float rad = P[2].x;
+    t = cand_sphere(lr, center_at(q0, q1, lr.time), rad);
+  } else if (type == PT_TRI) {
+    const float4 q1v = P[1], q2v = P[2];
+    const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
+    t = cand_tri(lr, q);
+  } else {
+    const float k = P[1].x;
+    if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
+    else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
+    else t = cand_rect<2>(lr, q0, k);
+  }
+  if (COUNT) { cnt[1]++; cnt[2 + type]++; }
+  // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
+  if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && meta.y > b.key))) {
+    b.t = t;
+    b.key = meta.y;
+    b.prim = (int32_t)pi;
+  }
+}
+
+// Conservative slab test on a padded box (culling only; never decides a hit).
+__device__ __forceinline__ bool slab_test(float lx, float ly, float lz, float hx, float hy, float hz,
+                                          V3 inv, V3 ood, float tmax_c, float& tnear) {
+  float tx0 = __builtin_fmaf(lx, inv.x, -ood.x), tx1 = __builtin_fmaf(hx, inv.x, -ood.x);
+  float ty0 = __builtin_fmaf(ly, inv.y, -ood.y), ty1 = __builtin_fmaf(hy, inv.y, -ood.y);
+  float tz0 = __builtin_fmaf(lz, inv.z, -ood.z), tz1 = __builtin_fmaf(hz, inv.z, -ood.z);
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_c));
+  tnear = tn;
+  return tn <= tf;
+}
+
+template <bool COUNT>
+__device__ Best trace(const DevScene& S, const Ray& r, int32_t* stk, uint32_t* cnt) {
+  Best b{INFINITY, 0u, -1};
+  uint32_t cur = 0;
+  Ray lr = r;
+  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT>(S, S.always[k], r, cur, lr, b, cnt);
+  if (S.n_nodes == 0) return b;
+  auto safe_inv = [](float d) {
+    float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
+    return __builtin_amdgcn_rcpf(dd);
+  };
+  const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+  const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
+  int32_t node = 0;
+  int sp = 0;
+  for (;;) {
+    const float4* N = reinterpret_cast<const float4*>(S.nodes + node);
+    const float4 n0 = N[0], n1 = N[1], n2 = N[2];
+    const int4 nc = *reinterpret_cast<const int4*>(N + 3);
+    if (COUNT) cnt[0]++;
+    const float tmax_c = __builtin_fmaf(b.t, 1.0e-5f, b.t) + 1.0e-5f;
+    float tn0, tn1;
+    bool h0 = slab_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, inv, ood, tmax_c, tn0);
+    bool h1 = nc.y >= 0 && slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1);
+    if (h0 && nc.z) {
+      for (int32_t k = 0; k < nc.z; ++k) test_prim<COUNT>(S, (uint32_t)(nc.x + k), r, cur, lr, b, cnt);
+      h0 = false;
+    }
+    if (h1 && nc.w) {
+      for (int32_t k = 0; k < nc.w; ++k) test_prim<COUNT>(S, (uint32_t)(nc.y + k), r, cur, lr, b, cnt);
+      h1 = false;
+    }
+    if (h0 && h1) {
+      const bool first0 = tn0 <= tn1;
+      stk[sp * BLOCK] = first0 ? nc.y : nc.x;
+      ++sp;
+      node = first0 ? nc.x : nc.y;
+    } else if (h0) {
+      node = nc.x;
+    } else if (h1) {
+      node = nc.y;
+    } else {
+      if (sp == 0) break;
+      --sp;
+      node = stk[sp * BLOCK];
+    }
+  }
+  return b;
+}
+
+// ---- hit record of the winner (hittable/mod.rs:32-48 at every level)
+struct Rec { V3 p, n; float u, v; bool front; uint32_t mat; };
+__device__ __forceinline__ void face(Rec& h, V3 dir, V3 outward) {
+  h.front = dot(dir, outward) < 0.0f;
+  h.n = h.front ? outward : neg(outward);
+}
+__device__ __forceinline__ void sphere_uv(V3 p, float& u, float& v) {  // spherical.rs:62-77
+  const float PI = 3.14159265358979323846f;
+  float theta = acosf(-p.y);
+  float phi = atan2f(-p.z, p.x) + PI;
+  u = phi / (2.0f * PI);
+  v = theta / PI;
+}
+
+__device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
+  const DevPrim P = S.prims[b.prim];
+  const uint32_t type = P.type_inst & 0xffu, inst = P.type_inst >> 8;
+  const DevInst* I = S.insts + inst;
+  const Ray lr = inst ? to_local(I, wr) : wr;
+  const float t = b.t;
+  Rec h;
+  h.mat = P.mat;
+  h.u = 0.0f;
+  h.v = 0.0f;
+  V3 outward;
+  h.p = add(lr.o, scale(lr.d, t));  // ray.rs:25-27
+  if (type == PT_SPHERE || type == PT_MSPHERE) {
+    V3 c = type == PT_SPHERE ? ld3(P.q0) : center_at(P.q0, P.q1, lr.time);
+    float rad = type == PT_SPHERE ? P.q0[3] : P.q2[0];
+    outward = divs(sub(h.p, c), rad);
+    if (S.mats[P.mat].needs_uv) sphere_uv(outward, h.u, h.v);
+  } else if (type == PT_TRI) {
+    const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
+                         P.q1[2], P.q1[3], P.q2[0], P.q2[1], P.q2[2], P.q2[3]};
+    TriUV s = tri_solve(lr, q);
+    const DevTriShade& sh = S.tshade[P.aux];
+    float w = 1.0f - s.u - s.v;  // triangular.rs:315-323
+    outward = add(add(scale(ld3(sh.n), w), scale(ld3(sh.n + 3), s.u)), scale(ld3(sh.n + 6), s.v));
+    h.u = (w * sh.uv[0] + s.u * sh.uv[2]) + s.v * sh.uv[4];
+    h.v = (w * sh.uv[1] + s.u * sh.uv[3]) + s.v * sh.uv[5];
+  } else {
+    const int axis = (int)type - PT_RECT_XY;
+    const float x = axis == 2 ? h.p.y : h.p.x;
+    const float y = axis == 0 ? h.p.y : h.p.z;
+    h.u = (x - P.q0[0]) / (P.q0[1] - P.q0[0]);
+    h.v = (y - P.q0[2]) / (P.q0[3] - P.q0[2]);
+    outward = axis == 0 ? mk(0.f, 0.f, 1.f) : (axis == 1 ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f));
+  }
+  face(h, lr.d, outward);
+  if (inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
+    for (int k = (int)I->nops - 1; k >= 0; --k) {
+      V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
+      for (int q = 0; q <= k; ++q) {
+        const float4 op = *reinterpret_cast<const float4*>(I->op[q]);
+        if (op.x == (float)IO_ROTY) dk = mk(op.z * dk.x - op.y * dk.z, dk.y, op.y * dk.x + op.z * dk.z);
+      }
+      const float4 op = *reinterpret_cast<const float4*>(I->op[k]);
+      if (op.x == (float)IO_TRANSLATE) {
+        h.p = add(h.p, mk(op.y, op.z, op.w));
+        face(h, dk, h.n);
+      } else {
+        const float s = op.y, c = op.z;
+        V3 p = mk(c * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + c * h.p.z);
+        V3 n = mk(c * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + c * h.n.z);
+        h.p = p;
+        face(h, dk, n);
+      }
+    }
+  }
+  return h;
+}
+
+// ---- textures (texture.rs:56-81, :97-104; image_texture.rs:34-52)
+__device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) {
+  for (int guard = 0; guard < 64; ++guard) {
+    const DevTex& t = S.texs[id];
+    if (t.type == TT_SOLID) return ld3(t.c);
+    if (t.type == TT_CHECKER) {
+      float sines = sinf(t.freq * p.x) * sinf(t.freq * p.y) * sinf(t.freq * p.z);
+      id = sines < 0.0f ? t.odd : t.even;
+      continue;
+    }
+    if (t.type == TT_IMAGE) {
+      float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+      float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+      float vv = 1.0f - vc;
+      float fi = uu * (float)t.w, fj = vv * (float)t.h;
+      uint32_t i = (fi != fi || fi <= 0.0f) ? 0u : (fi >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fi);
+      uint32_t j = (fj != fj || fj <= 0.0f) ? 0u : (fj >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fj);
+      i = i > t.w - 1 ? t.w - 1 : i;
+      j = j > t.h - 1 ? t.h - 1 : j;
+      const uint8_t* px = S.texels + t.off + ((size_t)j * t.w + i) * 3;
+      const float sc = 1.0f / 255.0f;
+      return mk((float)px[0] * sc, (float)px[1] * sc, (float)px[2] * sc);
+    }
+    return mk(u, v, 0.0f);  // UVDebug
+  }
+  return mk(0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // material.rs:108-112
+  float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+  r0 = r0 * r0;
+  float x = 1.0f - cosine;
+  float x2 = x * x;
+  return r0 + (1.0f - r0) * (x * (x2 * x2));  // powi(5) as LLVM expands it
+}
+
+// ---- the megakernel
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
+  __shared__ int32_t stk_all[STACK * BLOCK];
+  int32_t* stk = stk_all + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t_local = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long nrays = 0;
+  bool valid = t_local < a.n_tiles;
+  uint32_t tile = 0, i = 0, row = 0;
+  if (valid) {
+    tile = a.tile_ids ? a.tile_ids[t_local] : t_local;
+    i = (tile % a.tiles_x) * 8u + (lane & 7u);
+    row = (tile / a.tiles_x) * 8u + (lane >> 3);
+    valid = i < a.w && row < a.h;  // also rejects ids past the last tile (row >= h)
+  }
+  if (valid) {
+    const DevScene& S = a.scene;
+    const DevCamera& C = a.cam;
+    const uint32_t j = a.h - 1u - row;
+    const uint64_t hp = splitmix64(a.seed_hash ^ (((uint64_t)j << 32) | i));
+    const float inv_w = (float)(a.w - 1u), inv_h = (float)(a.h - 1u);
+    const V3 bg = ld3(a.bg);
+    V3 sum = mk(0.f, 0.f, 0.f);
+    uint32_t s = 0;
+    bool fresh = true;
+    uint64_t rng = 0;
+    Ray ray;
+    V3 T = mk(1.f, 1.f, 1.f);
+    uint32_t depth = 0;
+    for (;;) {
+      if (fresh) {  // lib.rs:83-86 + camera.rs:66-74
+        if (s == a.spp) break;
+        rng = splitmix64(hp ^ (uint64_t)s);
+        const float u = ((float)i + gen_f32(rng)) / inv_w;
+        const float v = ((float)j + gen_f32(rng)) / inv_h;
+        const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
+        const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
+        ray.o = add(ld3(C.origin), off);
+        ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)),
+                        ld3(C.origin)),
+                    off);
+        ray.time = gen_range(rng, C.time0, C.time1);
+        T = mk(1.f, 1.f, 1.f);
+        depth = a.max_depth;
+        fresh = false;
+        if (depth == 0) { ++s; fresh = true; continue; }
+      }
+      ++nrays;
+      const Best b = trace<COUNT>(S, ray, stk, cnt);
+      bool done = false;
+      V3 L = mk(0.f, 0.f, 0.f);
+      if (b.prim < 0) {  // lib.rs:102-105
+        L = mul(T, bg);
+        done = true;
+      } else {
+        const Rec h = hit_record(S, ray, b);
+        const DevMat& m = S.mats[h.mat];
+        if (m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
+          L = mul(T, tex_value(S, m.tex, h.u, h.v, h.p));
+          done = true;
+        } else if (m.type == MT_LAMBERT) {  // material.rs:42-56
+          V3 dir = add(h.n, unit(rand_in_unit_sphere(rng)));
+          if (near_zero(dir)) dir = h.n;
+          T = mul(T, tex_value(S, m.tex, h.u, h.v, h.p));
+          ray.o = h.p;
+          ray.d = dir;
+        } else if (m.type == MT_METAL) {  // material.rs:78-95
+          V3 refl = reflect(unit(ray.d), h.n);
+          V3 dir = add(refl, scale(rand_in_unit_sphere(rng), m.param));
+          if (dot(dir, h.n) > 0.0f) {
+            T = mul(T, ld3(m.albedo));
+            ray.o = h.p;
+            ray.d = dir;
+          } else {
+            done = true;  // absorbed: emitted() is black
+          }
+        } else {  // Dielectric, material.rs:116-142
+          const float ratio = h.front ? 1.0f / m.param : m.param;
+          const V3 ud = unit(ray.d);
+          const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
+          const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+          const bool cannot = (ratio * sin_t) > 1.0f;
+          V3 dir;
+          if (cannot || reflectance(cos_t, ratio) > gen_f32(rng)) dir = reflect(ud, h.n);
+          else dir = refract(ud, h.n, ratio);
+          ray.o = h.p;
+          ray.d = dir;  // attenuation (1,1,1): T unchanged
+        }
+        if (!done && --depth == 0) done = true;  // lib.rs:98-100
+      }
+      if (done) {
+        sum = add(sum, L);
+        ++s;
+        fresh = true;
+      }
+    }
+    float* o = a.tile_ids ? a.out + ((size_t)t_local * 64u + lane) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
+    o[0] = sum.x;
+    o[1] = sum.y;
+    o[2] = sum.z;
+  }
+  // one atomic per wave for the ray counter
+  unsigned long long tot = nrays;
+  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+  if (lane == 0 && tot) atomicAdd(a.counters, tot);
+  if (COUNT) {
+    for (int q = 0; q < 8; ++q) {
+      unsigned long long c = cnt[q];
+      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+      if (lane == 0 && c) atomicAdd(a.counters + 1 + q, c);
+    }
+  }
+}
+
+__global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
+                                    uint32_t n_tiles, const float* packed, float* img) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_tiles * 64u) return;
+  const uint32_t t = g >> 6, lane = g & 63u, tile = tiles[t];
+  const uint32_t i = (tile % tiles_x) * 8u + (lane & 7u), row = (tile / tiles_x) * 8u + (lane >> 3);
+  if (i >= w || row >= h) return;
+  for (int c = 0; c < 3; ++c) img[((size_t)row * w + i) * 3 + c] = packed[(size_t)g * 3 + c];
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------- host side
+static int hip_fail(hipError_t e, const char* what) {
+  return fail(RTW_ENODEV, "%s: %s", what, hipGetErrorString(e));
+}
+#define HIPCHK(x, what)                          \
+  do {                                           \
+    hipError_t e_ = (x);                         \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+template <class T>
+static size_t put(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+  size_t off = (blob.size() + 255) & ~(size_t)255;
+  blob.resize(off + sizeof(T) * v.size());
+  if (!v.empty()) memcpy(blob.data() + off, v.data(), sizeof(T) * v.size());
+  return off;
+}
+
+int upload(Scene& s, int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(RTW_ENODEV, "no HIP device visible (the render core has no CPU fallback)");
+  if (device >= ndev) return fail(RTW_EINVAL, "device %d >= device count %d", device, ndev);
+  const Flat& f = s.flat;
+  std::vector<uint8_t> blob;
+  size_t o_nodes = put(blob, f.nodes), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
+  size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
+  size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels);
+  blob.resize((blob.size() + 255) & ~(size_t)255);
+  int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
+  int prev = 0;
+  hipGetDevice(&prev);
+  for (int d = d0; d < d1; ++d) {
+    HIPCHK(hipSetDevice(d), "hipSetDevice");
+    DeviceCopy c;
+    c.device = d;
+    c.bytes = blob.size();
+    HIPCHK(hipMalloc(&c.block, c.bytes), "hipMalloc(scene)");
+    HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
+    HIPCHK(hipMalloc((void**)&c.counters, 16 * sizeof(unsigned long long)), "hipMalloc(counters)");
+    uint8_t* base = (uint8_t*)c.block;
+    c.scene.nodes = (const DevNode*)(base + o_nodes);
+    c.scene.prims = (const DevPrim*)(base + o_prims);
+    c.scene.always = (const uint32_t*)(base + o_always);
+    c.scene.tshade = (const DevTriShade*)(base + o_tsh);
+    c.scene.insts = (const DevInst*)(base + o_inst);
+    c.scene.mats = (const DevMat*)(base + o_mat);
+    c.scene.texs = (const DevTex*)(base + o_tex);
+    c.scene.texels = (const uint8_t*)(base + o_texel);
+    c.scene.n_nodes = (uint32_t)f.nodes.size();
+    c.scene.n_prims = (uint32_t)f.prims.size();
+    c.scene.n_always = (uint32_t)f.always.size();
+    c.scene.n_insts = (uint32_t)f.insts.size();
+    s.dev.push_back(c);
+  }
+  hipSetDevice(prev);
+  return RTW_OK;
+}
+
+void release(Scene& s) {
+  for (DeviceCopy& c : s.dev) {
+    if (hipSetDevice(c.device) != hipSuccess) continue;
+    if (c.block) hipFree(c.block);
+    if (c.counters) hipFree(c.counters);
+  }
+  s.dev.clear();
+}
+
+static DeviceCopy* find_copy(Scene& s, int device) {
+  for (DeviceCopy& c : s.dev)
+    if (c.device == device || device < 0) return &c;
+  return nullptr;
+}
+
+static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w,
+                  uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
+                  uint32_t n_tiles, float* d_out, hipStream_t stream, uint32_t flags, hipEvent_t ev0,
+                  hipEvent_t ev1) {
+  if (cam->time0 < sc.flat.time_lo || cam->time1 > sc.flat.time_hi)
+    return fail(RTW_EINVAL, "camera shutter [%g, %g) outside the committed motion range [%g, %g]",
+                cam->time0, cam->time1, sc.flat.time_lo, sc.flat.time_hi);
+  RenderArgs a;
+  memset(&a, 0, sizeof a);
+  a.scene = c.scene;
+  memcpy(a.cam.origin, cam->origin, sizeof a.cam.origin);
+  memcpy(a.cam.llc, cam->lower_left_corner, sizeof a.cam.llc);
+  memcpy(a.cam.horizontal, cam->horizontal, sizeof a.cam.horizontal);
+  memcpy(a.cam.vertical, cam->vertical, sizeof a.cam.vertical);
+  memcpy(a.cam.u, cam->u, sizeof a.cam.u);
+  memcpy(a.cam.v, cam->v, sizeof a.cam.v);
+  a.cam.lens_radius = cam->lens_radius;
+  a.cam.time0 = cam->time0;
+  a.cam.time1 = cam->time1;
+  memcpy(a.bg, bg, sizeof a.bg);
+  a.w = w; a.h = h; a.spp = spp; a.max_depth = max_depth;
+  a.tiles_x = (w + 7u) / 8u;
+  a.n_tiles = n_tiles;
+  a.tile_ids = d_tiles;
+  // the host mirror of dev::splitmix64 (seed pre-hash shared by every pixel)
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  a.seed_hash = z ^ (z >> 31);
+  a.out = d_out;
+  a.counters = c.counters;
+  HIPCHK(hipMemsetAsync(c.counters, 0, 16 * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  const uint32_t waves_per_block = dev::BLOCK / 64;
+  dim3 grid((n_tiles + waves_per_block - 1) / waves_per_block), block(dev::BLOCK);
+  if (ev0) HIPCHK(hipEventRecord(ev0, stream), "hipEventRecord");
+  if (n_tiles) {
+    if (flags & RTW_FLAG_COUNT_TRAVERSAL)
+      hipLaunchKernelGGL(dev::render_kernel<true>, grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL(dev::render_kernel<false>, grid, block, 0, stream, a);
+    HIPCHK(hipGetLastError(), "render_kernel launch");
+  }
+  if (ev1) HIPCHK(hipEventRecord(ev1, stream), "hipEventRecord");
+  return RTW_OK;
+}
+
+static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1, uint64_t paths,
+                      rtw_stats* st) {
+  HIPCHK(hipStreamSynchronize(stream), "render_kernel");
+  unsigned long long cnt[16];
+  HIPCHK(hipMemcpy(cnt, c.counters, sizeof cnt, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
+  float ms = 0.f;
+  if (ev0 && ev1) HIPCHK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
+  st->rays = cnt[0];
+  st->paths = paths;
+  st->kernel_ms = ms;
+  st->node_visits = cnt[1];
+  st->prim_tests = cnt[2];
+  for (int k = 0; k < 6; ++k) st->prim_tests_by_type[k] = cnt[3 + k];
+  return RTW_OK;
+}
+
+}  // namespace rtw
+
+using namespace rtw;
+
+extern "C" {
+
+int rtw_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
+               uint32_t spp, uint32_t max_depth, uint64_t seed, float* out, rtw_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!s || !cam || !bg || !out) return fail(RTW_EINVAL, "NULL argument");
+  if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
+  if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2 (lib.rs:84-85 divides by w-1, h-1)");
+  DeviceCopy* c = find_copy(s->s, -1);
+  if (!c) return fail(RTW_ENODEV, "scene has no device copy");
+  int prev = 0;
+  hipGetDevice(&prev);
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+  float* d_out = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = RTW_OK;
+  if (hipMalloc(&d_out, bytes) != hipSuccess) { hipSetDevice(prev); return fail(RTW_ENOMEM, "hipMalloc(image)"); }
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const uint32_t n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
+  rtw_stats st;
+  memset(&st, 0, sizeof st);
+  rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, nullptr, n_tiles, d_out, nullptr, 0, e0, e1);
+  if (rc == RTW_OK) rc = fill_stats(*c, nullptr, e0, e1, (uint64_t)w * h * spp, &st);
+  if (rc == RTW_OK && hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(RTW_ENODEV, "hipMemcpy(image)");
+  hipFree(d_out);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipSetDevice(prev);
+  st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) *stats = st;
+  return rc;
+}
+
+int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w,
+                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
+                      uint32_t n_tiles, float* d_out, void* stream_, uint32_t flags, rtw_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!s || !cam || !bg || !d_out) return fail(RTW_EINVAL, "NULL argument");
+  if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
+  if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2");
+  DeviceCopy* c = find_copy(s->s, device);
+  if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
+  if (!d_tiles) n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
+  int prev = 0;
+  hipGetDevice(&prev);
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t stream = (hipStream_t)stream_;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (stats) { hipEventCreate(&e0); hipEventCreate(&e1); }
+  int rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_tiles, n_tiles, d_out, stream, flags, e0, e1);
+  if (rc == RTW_OK && stats) {
+    rtw_stats st;
+    memset(&st, 0, sizeof st);
+    rc = fill_stats(*c, stream, e0, e1, (uint64_t)n_tiles * 64u * spp, &st);
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *stats = st;
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipSetDevice(prev);
+  return rc;
+}
+
+int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_tiles,
+                            const float* d_packed, float* d_image, void* stream) {
+  if (!d_tiles || !d_packed || !d_image) return fail(RTW_EINVAL, "NULL argument");
+  int prev = 0;
+  hipGetDevice(&prev);
+  if (device >= 0) HIPCHK(hipSetDevice(device), "hipSetDevice");
+  const uint32_t n = n_tiles * 64u;
+  if (n) {
+    hipLaunchKernelGGL(dev::unpack_tiles_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, h,
+                       (w + 7u) / 8u, d_tiles, n_tiles, d_packed, d_image);
+    hipError_t e = hipGetLastError();
+    hipSetDevice(prev);
+    if (e != hipSuccess) return hip_fail(e, "unpack_tiles_kernel");
+  }
+  hipSetDevice(prev);
+  return RTW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// rtw_scene.hpp — host-side scene graph behind the rtw_* builder calls.
+//
+// The graph keeps the reference's Hittable tree shape (raytracer_weekend_lib/src/hittable/,
+// bvh.rs) so that rtw_scene_dump() can hand the exact hierarchy to the test oracle; the
+// flattener (rtw_flatten.cpp) turns it into the device layout of rtw_device.hpp.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "rtw_device.hpp"
+
+struct rtw_scene;  // opaque in the C-ABI; defined below as rtw::Scene's holder
+
+namespace rtw {
+
+enum NodeKind : uint32_t {
+  NK_LIST,       // Vec<Box<dyn Hittable>>              hittable/mod.rs:57-69
+  NK_BVH,        // BvhNode::new(objects, t0, t1)       bvh.rs:19-74 (set semantics)
+  NK_TRANSLATE,  // Translation                         transformations.rs:16-47
+  NK_ROTY,       // YRotation                           transformations.rs:50-148
+  NK_SPHERE,     // Sphere                              spherical.rs:79-104
+  NK_MSPHERE,    // MovingSphere                        spherical.rs:106-151
+  NK_RECT,       // XY/XZ/YZRectangle                   rectangular.rs:16-166
+  NK_CUBOID,     // Cuboid (six rects)                  rectangular.rs:170-245
+  NK_TRI,        // Triangle                            triangular.rs:33-149
+};
+
+struct Node {
+  NodeKind kind;
+  std::vector<uint32_t> ch;  // children (groups / wrappers)
+  float f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t axis = 0, mat = 0, tri = 0;
+  float sin_t = 0.f, cos_t = 1.f;  // YRotation, computed as transformations.rs:60-63
+};
+
+struct TexH {
+  uint32_t type = TT_SOLID, odd = 0, even = 0;
+  float c[3] = {0, 0, 0};
+  float freq = 0.f;
+  uint32_t w = 0, h = 0;
+  std::vector<uint8_t> img;
+};
+
+struct MatH {
+  uint32_t type = MT_LAMBERT, tex = 0;
+  float albedo[3] = {0, 0, 0};
+  float param = 0.f;
+};
+
+// Flattened host copy of what goes to every device.
+struct Flat {
+  std::vector<DevNode> nodes;
+  std::vector<DevPrim> prims;
+  std::vector<uint32_t> always;
+  std::vector<DevTriShade> tshade;
+  std::vector<DevInst> insts;
+  std::vector<DevMat> mats;
+  std::vector<DevTex> texs;
+  std::vector<uint8_t> texels;
+  uint32_t depth = 0;
+  float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover
+};
+
+struct DeviceCopy {
+  int device = -1;
+  void* block = nullptr;  // one hipMalloc holding every table
+  size_t bytes = 0;
+  DevScene scene{};
+  unsigned long long* counters = nullptr;  // 16 x u64
+};
+
+struct Scene {
+  std::vector<TexH> tex;
+  std::vector<MatH> mat;
+  std::vector<Node> nodes;        // nodes[0] = world list
+  std::vector<uint32_t> open{0};  // open-group stack
+  std::vector<float> tri_v, tri_n, tri_uv;  // per triangle: 9, 9, 6 floats (raw inputs)
+  std::vector<uint8_t> tri_nm, tri_uvm;     // per triangle: normal / uv presence masks
+  bool committed = false;
+  Flat flat;
+  std::vector<DeviceCopy> dev;
+  Scene() { nodes.push_back(Node{NK_LIST, {}}); }
+};
+
+// rtw_flatten.cpp
+int flatten(Scene& s);
+// rtw_scene.cpp
+std::string dump_scene(const Scene& s);
+// rtw_kernel.hip
+int upload(Scene& s, int device);
+void release(Scene& s);
+
+// thread-local error reporting (rtw_capi.cpp)
+int fail(int code, const char* fmt, ...);
+
+}  // namespace rtw
+
+struct rtw_scene {
+  rtw::Scene s;
+};
