@@ -124,7 +124,7 @@ class OracleScene:
         out = np.zeros((h, w, 3), np.float32)
         rays = C.c_uint64()
         r = np.ascontiguousarray(rows, np.uint32) if rows is not None else None
-        n = threads or os.cpu_count() or 1
+        n = threads or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
         rc = lib().oracle_render(self._p, C.byref(cam), fp(f32(background)), w, h, spp, max_depth, seed,
                                  integrator, bvh_mode, n, r.ctypes.data_as(_U32) if r is not None else None,
                                  len(r) if r is not None else 0, fp(out), C.byref(rays))

@@ -118,7 +118,7 @@ typedef struct {
   uint32_t n, used;
 } draws;
 static inline uint32_t next_u32(draws* d) {
-  if (d->arr) { uint32_t v = d->used < d->n ? d->arr[d->used] : 0u; d->used++; return v; }
+  if (d->arr) { uint32_t v = d->used < d->n ? d->arr[d->used] : 0x80000000u; d->used++; return v; }  /* exhausted -> 0.0 in [-1,1) */
   d->used++;
   return pcg_next(&d->rng);
 }

@@ -116,6 +116,14 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             raise RtwError(RTW_ENODEV, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        # torch-ROCm bundles its own libamdhip64.so.7 + libhsa-runtime64 under the same SONAME as
+        # /opt/rocm's; whichever loads first serves the whole process.  Load torch's first so the
+        # render core and torch's streams / RCCL share ONE HIP runtime (the other order leaves torch
+        # with "No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)

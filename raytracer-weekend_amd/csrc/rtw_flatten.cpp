@@ -413,7 +413,7 @@ int flatten(Scene& s) {
         nd.b1lo[a] = INFINITY; nd.b1hi[a] = -INFINITY;
       }
       nd.c0 = root.idx; nd.n0 = root.count;
-      nd.c1 = 0; nd.n1 = 0;
+      nd.c1 = -1; nd.n1 = 0;  // no second child (the kernel tests c1 >= 0)
       f.nodes.push_back(nd);
     }
     f.depth = bb.max_depth;
@@ -424,6 +424,32 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // structural self-check: every internal node reached exactly once from the root, every
+  // leaf range inside the BVH part of prims[], every BVH prim covered exactly once
+  if (!f.nodes.empty()) {
+    std::vector<uint8_t> seen_node(f.nodes.size(), 0), seen_prim(rest.size(), 0);
+    std::vector<int32_t> todo{0};
+    seen_node[0] = 1;
+    while (!todo.empty()) {
+      const DevNode nd = f.nodes[todo.back()];
+      todo.pop_back();
+      const int32_t c[2] = {nd.c0, nd.c1};
+      const uint32_t n[2] = {nd.n0, nd.n1};
+      for (int k = 0; k < 2; ++k) {
+        if (c[k] < 0 && n[k] == 0) continue;  // absent child
+        if (n[k]) {
+          if (c[k] < 0 || (size_t)c[k] + n[k] > rest.size()) return fail(RTW_EINVAL, "BVH leaf out of range");
+          for (uint32_t q = 0; q < n[k]; ++q)
+            if (seen_prim[c[k] + q]++) return fail(RTW_EINVAL, "BVH prim referenced twice");
+        } else {
+          if ((size_t)c[k] >= f.nodes.size() || seen_node[c[k]]++) return fail(RTW_EINVAL, "BVH node cycle/range");
+          todo.push_back(c[k]);
+        }
+      }
+    }
+    for (uint8_t x : seen_prim)
+      if (!x) return fail(RTW_EINVAL, "BVH misses a primitive");
+  }
   return RTW_OK;
 }
 

@@ -240,7 +240,8 @@ __device__ Best trace(const DevScene& S, const Ray& r, int32_t* stk, uint32_t* c
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
   int32_t node = 0;
   int sp = 0;
-  for (;;) {
+  // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
+  for (uint32_t guard = 0; guard < (1u << 22); ++guard) {
     const float4* N = reinterpret_cast<const float4*>(S.nodes + node);
     const float4 n0 = N[0], n1 = N[1], n2 = N[2];
     const int4 nc = *reinterpret_cast<const int4*>(N + 3);
@@ -259,8 +260,7 @@ __device__ Best trace(const DevScene& S, const Ray& r, int32_t* stk, uint32_t* c
     }
     if (h0 && h1) {
       const bool first0 = tn0 <= tn1;
-      stk[sp * BLOCK] = first0 ? nc.y : nc.x;
-      ++sp;
+      if (sp < STACK) stk[(sp++) * BLOCK] = first0 ? nc.y : nc.x;  // depth <= 31: never dropped
       node = first0 ? nc.x : nc.y;
     } else if (h0) {
       node = nc.x;

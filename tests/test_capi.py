@@ -1,0 +1,120 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/rtw.h
+declares, builder errors match the reference's panics, host-side pieces (camera, tonemap,
+flattener) agree with the oracle.  Nothing here launches a kernel."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def header_functions():
+    text = (ROOT / "include" / "rtw.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtw_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported(rtw):
+    lib = rtw.lib()
+    declared = header_functions()
+    assert len(declared) >= 30
+    missing = [f for f in declared if not hasattr(lib, f)]
+    assert not missing, missing
+    assert set(declared) == set(rtw.EXPORTED_SYMBOLS), set(declared) ^ set(rtw.EXPORTED_SYMBOLS)
+    assert lib.rtw_abi_version() == 1
+
+
+def test_camera_matches_oracle(rtw, orc):
+    """camera.rs:25-64 restated twice (product host C++ vs oracle C): bit-identical."""
+    cases = [((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, 16 / 9, 0.1, 10.0),
+             ((278, 278, -800), (278, 278, 0), (0, 1, 0), 40.0, 1.0, 0.0, 10.0),
+             ((-5, -30, 25), (0, 0, 5), (1, 0, 0), 40.0, 3840 / 2160, 0.0, 10.0),
+             ((0.5, 2.5, 0.8), (-0.1, 2.3, 0.15), (0, 1, 0), 40.0, 1.3, 0.5, 3.3)]
+    for a in cases:
+        p = rtw.Camera.new(*a).as_dict()
+        o = orc.camera_new(*a)
+        for k, _ in orc.oracle_camera._fields_:
+            pv = np.asarray(p[k], np.float32)
+            ov = np.asarray(list(getattr(o, k)) if isinstance(p[k], list) else getattr(o, k), np.float32)
+            assert np.array_equal(pv.view(np.uint32), ov.view(np.uint32)), (a, k, pv, ov)
+
+
+def test_camera_rejects_empty_shutter(rtw):
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.Camera.new((0, 0, 1), (0, 0, 0), (0, 1, 0), 40, 1, 0, 1, 0.5, 0.5)  # gen_range panics on empty
+    assert e.value.code == rtw.RTW_EINVAL
+
+
+def test_tonemap_matches_oracle(rtw, orc):
+    rng = np.random.default_rng(1)
+    sums = np.concatenate([rng.uniform(-1, 60, 3000), [np.nan, np.inf, -np.inf, 0, 50]]).astype(np.float32)
+    sums = sums[: (len(sums) // 3) * 3].reshape(-1, 3)
+    got = rtw.tonemap(sums, 50)
+    want = np.array([[orc.lib().oracle_tonemap(float(x), 50) for x in row] for row in sums], np.uint8)
+    assert np.array_equal(got, want)
+
+
+def test_metal_fuzz_assert(rtw):
+    s = rtw.Scene()
+    s.metal((0.5, 0.5, 0.5), 1.0)
+    with pytest.raises(rtw.RtwError) as e:
+        s.metal((0.5, 0.5, 0.5), 1.01)  # material.rs:71 assert!(fuzz <= 1.0)
+    assert e.value.code == rtw.RTW_EINVAL
+
+
+def test_builder_errors(rtw):
+    s = rtw.Scene()
+    with pytest.raises(rtw.RtwError):
+        s.sphere((0, 0, 0), 1, 7)  # no such material
+    with pytest.raises(rtw.RtwError):
+        s.checker(0, 1, 10)  # no such textures
+    assert rtw.lib().rtw_end(s._p) == rtw.RTW_ESTATE  # no open group
+    m = s.lambertian_solid((0.5, 0.5, 0.5))
+    assert rtw.lib().rtw_begin_translate(s._p, 1, 2, 3) == 0
+    with pytest.raises(rtw.RtwError) as e:  # a group is still open
+        s.commit()
+    assert e.value.code == rtw.RTW_ESTATE
+    assert rtw.lib().rtw_end(s._p) == 0
+    assert rtw.lib().rtw_end(s._p) == rtw.RTW_ESTATE  # nothing open
+    with pytest.raises(rtw.RtwError) as e:
+        rtw.Scene().load_wavefront_obj("/nonexistent.obj")
+    assert e.value.code == rtw.RTW_EIO
+    del m
+
+
+@pytest.mark.parametrize("name", ["jumpy-balls", "cornell-box", "wavefront-cow-obj", "textured-monument",
+                                  "two-spheres", "simple-triangle"])
+def test_flatten_self_check(rtw, name):
+    """rtw_scene_commit flattens + builds the BVH (with its structural self-check) before it
+    needs a device; on a GPU-less host the only acceptable failure is RTW_ENODEV."""
+    s = rtw.Scene()
+    s.preset(name, 16 / 9, seed=3)
+    leaves = s.info(0)
+    if rtw.device_count() > 0:
+        s.commit()
+    else:
+        with pytest.raises(rtw.RtwError) as e:
+            s.commit()
+        assert e.value.code == rtw.RTW_ENODEV, str(e.value)
+    nodes, depth, always = s.info(3), s.info(4), s.info(5)
+    assert depth <= 31 and nodes >= 1
+    if name == "jumpy-balls":
+        assert always == 1  # the r=1000 ground sphere is tested for every ray, not in the BVH
+        assert nodes < 2 * leaves
+
+
+def test_presets_unknown_scene(rtw):
+    s = rtw.Scene()
+    with pytest.raises(rtw.RtwError) as e:
+        s.preset("book2-final-scene", 1.0)
+    assert "out-of-scope" in str(e.value)
+
+
+def test_image_height_rule(rtw):
+    """console_app/src/main.rs:33: round(width / 1.7777778)."""
+    assert rtw.image_height(400) == 225
+    assert rtw.image_height(1920) == 1080
+    assert rtw.image_height(3840) == 2160
+    assert rtw.camera_aspect(1920, 1080) == np.float32(1920) / np.float32(1080)

@@ -1,0 +1,95 @@
+"""World-size-2 frame partition + gather on CPU (gloo): the N>1 path of bench.py.
+
+Each rank "renders" its tiles with a deterministic stand-in (pixel value = f(row, col)),
+packs them as rtw_render_device does, all-gathers, and rank 0 unpacks with the index math
+of unpack_tiles_kernel; the result must equal the single-rank frame for ragged sizes."""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def fake_pixel(row, col):
+    return np.stack([row * 1000.0 + col, row + 0.5, col * 0.25], -1).astype(np.float32)
+
+
+def unpack(w, h, ids, packed):
+    """CPU restatement of unpack_tiles_kernel (rtw_kernel.hip) for the test."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from conftest import load_rtw
+    T = load_rtw()
+    import importlib
+    tiles = importlib.import_module("rtw_amd.tiles")
+    img = np.zeros((h, w, 3), np.float32)
+    for slot, t in enumerate(ids):
+        if t >= tiles.n_tiles(w, h):
+            continue
+        r, c = tiles.tile_pixels(int(t), w, h)
+        ok = (r < h) & (c < w)
+        img[r[ok], c[ok]] = packed[slot][ok]
+    return img
+
+
+def worker(rank, world, w, h, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, str(ROOT / "tests"))
+    from conftest import load_rtw
+    load_rtw()
+    import importlib
+    tiles = importlib.import_module("rtw_amd.tiles")
+    nt = tiles.n_tiles(w, h)
+    pr = tiles.per_rank(nt, world)
+    mine = tiles.rank_tiles(nt, world, rank)
+    packed = np.zeros((pr, 64, 3), np.float32)
+    for k, t in enumerate(mine):
+        r, c = tiles.tile_pixels(int(t), w, h)
+        packed[k] = fake_pixel(r, c)
+    out = torch.zeros((world * pr, 64, 3))
+    dist.all_gather_into_tensor(out, torch.from_numpy(packed))
+    if rank == 0:
+        img = unpack(w, h, tiles.gather_layout(nt, world), out.numpy())
+        q.put(img)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("w,h", [(72, 40), (64, 64), (17, 9)])
+def test_two_rank_gather_rebuilds_frame(w, h):
+    import torch.multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=worker, args=(r, 2, w, h, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rows, cols = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    assert np.array_equal(img, fake_pixel(rows, cols))
+
+
+def test_partition_covers_every_tile_once():
+    sys.path.insert(0, str(ROOT / "tests"))
+    from conftest import load_rtw
+    load_rtw()
+    import importlib
+    tiles = importlib.import_module("rtw_amd.tiles")
+    for nt in (1, 7, 32400):
+        for world in (1, 2, 3, 8):
+            lay = tiles.gather_layout(nt, world)
+            real = np.sort(lay[lay < nt])
+            assert np.array_equal(real, np.arange(nt))
+            sizes = [len(tiles.rank_tiles(nt, world, r)) for r in range(world)]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,65 @@
+"""The oracle's two integrators and two BVH modes agree.
+
+ITERATIVE (L = T * terminal, T = ((a0*a1)*a2)...) is what the GPU computes bit-for-bit;
+RECURSIVE is lib.rs:97-117 literally (emitted + a0 * (a1 * (...))).  They draw the same
+random numbers and trace the same paths, so they differ only in the rounding of the
+throughput product: a few ulp per bounce.  Tolerance: relative 2e-5 per pixel component,
+far inside the north_star's RMSE < 1e-4 on the mean image.
+BVH_REFERENCE builds bvh.rs:19-74's tree (random axis, median split) and walks it as
+bvh.rs:100-120 does; BVH_AS_LIST is the set semantics the GPU reproduces.  They agree
+except on exact t ties between triangles, so the images must match to the same tolerance.
+"""
+import numpy as np
+import pytest
+
+
+def scene(rtw, orc, name, seed=3):
+    s = rtw.Scene()
+    cam, bg = s.preset(name, 16 / 9, seed=seed)
+    return orc.OracleScene(s.dump(), s.images()), orc.camera_from_fields(cam.as_dict()), bg
+
+
+@pytest.mark.parametrize("name,w,h,spp", [("jumpy-balls", 48, 27, 4), ("cornell-box", 32, 18, 8),
+                                          ("wavefront-cow-obj", 32, 18, 2)])
+def test_recursive_vs_iterative(rtw, orc, name, w, h, spp):
+    o, cam, bg = scene(rtw, orc, name)
+    a, ra = o.render(cam, bg, w, h, spp, seed=4, integrator=orc.ITERATIVE)
+    b, rb = o.render(cam, bg, w, h, spp, seed=4, integrator=orc.RECURSIVE)
+    assert ra == rb
+    assert np.allclose(a, b, rtol=2e-5, atol=1e-6)
+    rmse = np.sqrt(np.mean((a / spp - b / spp) ** 2))
+    assert rmse < 1e-6
+
+
+def test_reference_bvh_vs_list(rtw, orc):
+    o, cam, bg = scene(rtw, orc, "wavefront-cow-obj")
+    a, ra = o.render(cam, bg, 40, 22, 2, seed=4, bvh_mode=orc.BVH_AS_LIST)
+    b, rb = o.render(cam, bg, 40, 22, 2, seed=4, bvh_mode=orc.BVH_REFERENCE)
+    assert ra == rb
+    assert np.allclose(a, b, rtol=2e-5, atol=1e-6)
+
+
+def test_threads_do_not_change_the_image(rtw, orc):
+    o, cam, bg = scene(rtw, orc, "jumpy-balls")
+    a, _ = o.render(cam, bg, 32, 18, 2, seed=8, threads=1)
+    b, _ = o.render(cam, bg, 32, 18, 2, seed=8, threads=7)
+    assert np.array_equal(a, b)
+
+
+def test_row_subset_matches_full(rtw, orc):
+    o, cam, bg = scene(rtw, orc, "jumpy-balls")
+    full, _ = o.render(cam, bg, 32, 18, 2, seed=8)
+    part, _ = o.render(cam, bg, 32, 18, 2, seed=8, rows=[17, 5, 0])
+    for j in (17, 5, 0):
+        assert np.array_equal(part[18 - 1 - j], full[18 - 1 - j])
+
+
+def test_estimator_converges(rtw, orc):
+    """Different seeds estimate the same mean image: RMSE shrinks ~ 1/sqrt(spp)."""
+    o, cam, bg = scene(rtw, orc, "cornell-box")
+    errs = []
+    for spp in (4, 64):
+        a, _ = o.render(cam, bg, 16, 9, spp, seed=1)
+        b, _ = o.render(cam, bg, 16, 9, spp, seed=2)
+        errs.append(np.sqrt(np.mean((a / spp - b / spp) ** 2)))
+    assert errs[1] < errs[0] / 2
