@@ -153,7 +153,7 @@ def main() -> int:
     host_image = torch.empty((h, w, 3), dtype=torch.float32, pin_memory=True) if rank == 0 else None
     stream = torch.cuda.current_stream()
 
-    launches = args.launches or max(1, min(64, n_mine // 4096))
+    launches = args.launches or 1  # persistent path kernel: one launch drains the whole frame
     bounds = np.linspace(0, n_mine, launches + 1).astype(int)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
 

@@ -98,11 +98,14 @@ struct RenderArgs {
   float bg[3];
   uint32_t w, h, spp, max_depth;
   uint32_t tiles_x;           // ceil(w / 8)
-  uint32_t n_tiles;           // tiles to render
-  const uint32_t* tile_ids;   // device array or nullptr (= tiles 0..n_tiles-1, full-image output)
+  uint32_t slot_base;         // first tile slot of this pass
+  const uint32_t* tile_ids;   // device array or nullptr (slot == tile id, full-image output)
   uint64_t seed_hash;         // splitmix64(seed)
+  uint64_t n_paths;           // paths in this pass = slots * 64 * spp
+  float* sbuf;                // ordered sample buffer: 3 planes of n_paths floats
   float* out;
   unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
+  unsigned long long* queue;     // path-id dispenser of this pass
 };
 
 }  // namespace rtw

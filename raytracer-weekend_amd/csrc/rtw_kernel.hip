@@ -21,6 +21,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 
 #include "../../include/rtw.h"
@@ -383,110 +384,157 @@ __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // 
   return r0 + (1.0f - r0) * (x * (x2 * x2));  // powi(5) as LLVM expands it
 }
 
-// ---- the megakernel
+// ---- the persistent path kernel
+//
+// Work unit = one path (pixel, sample).  Path id p (within a pass) = (slot*spp + s)*64 + l:
+// slot = tile slot, s = sample, l = lane-in-tile, so the 64 paths a wave draws together
+// are one sample of one 8x8 tile (coherent camera rays).  Waves are persistent: whenever
+// lanes finish a path, the wave hands them new ids from a per-wave pool (ballot + mbcnt
+// prefix), refilled from a global counter BATCH ids at a time, so lanes stay busy and the
+// grid drains with a one-path tail.  Each finished path writes L to the ordered sample
+// buffer (SoA planes, 12 B/path in HBM); reduce_kernel then sums each pixel's samples in
+// sample order — exactly lib.rs:83-87's `pixel_color += sample_ray(..)` sequence.
+constexpr uint32_t BATCH = 256;
+
+struct PathState {
+  Ray ray;
+  V3 T;
+  uint64_t rng;
+  uint64_t pid;
+  uint32_t depth;
+};
+
+__device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {
+  const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
+  const uint32_t slot = hi / a.spp, s = hi - slot * a.spp;
+  const uint32_t gslot = a.slot_base + slot;
+  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
+  const uint32_t i = (tile % a.tiles_x) * 8u + (l & 7u), row = (tile / a.tiles_x) * 8u + (l >> 3);
+  if (i >= a.w || row >= a.h) return false;
+  const uint32_t j = a.h - 1u - row;
+  const DevCamera& C = a.cam;
+  uint64_t rng = splitmix64(splitmix64(a.seed_hash ^ (((uint64_t)j << 32) | i)) ^ (uint64_t)s);
+  // lib.rs:84-86 + camera.rs:66-74
+  const float u = ((float)i + gen_f32(rng)) / (float)(a.w - 1u);
+  const float v = ((float)j + gen_f32(rng)) / (float)(a.h - 1u);
+  const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
+  const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
+  st.ray.o = add(ld3(C.origin), off);
+  st.ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)), ld3(C.origin)),
+                 off);
+  st.ray.time = gen_range(rng, C.time0, C.time1);
+  st.rng = rng;
+  st.T = mk(1.f, 1.f, 1.f);
+  st.depth = a.max_depth;
+  st.pid = pid;
+  return true;
+}
+
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
+__global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
   __shared__ int32_t stk_all[STACK * BLOCK];
   int32_t* stk = stk_all + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t t_local = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const DevScene& S = a.scene;
+  const V3 bg = ld3(a.bg);
+  const uint64_t P = a.n_paths;
   uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
-  bool valid = t_local < a.n_tiles;
-  uint32_t tile = 0, i = 0, row = 0;
-  if (valid) {
-    tile = a.tile_ids ? a.tile_ids[t_local] : t_local;
-    i = (tile % a.tiles_x) * 8u + (lane & 7u);
-    row = (tile / a.tiles_x) * 8u + (lane >> 3);
-    valid = i < a.w && row < a.h;  // also rejects ids past the last tile (row >= h)
-  }
-  if (valid) {
-    const DevScene& S = a.scene;
-    const DevCamera& C = a.cam;
-    const uint32_t j = a.h - 1u - row;
-    const uint64_t hp = splitmix64(a.seed_hash ^ (((uint64_t)j << 32) | i));
-    const float inv_w = (float)(a.w - 1u), inv_h = (float)(a.h - 1u);
-    const V3 bg = ld3(a.bg);
-    V3 sum = mk(0.f, 0.f, 0.f);
-    uint32_t s = 0;
-    bool fresh = true;
-    uint64_t rng = 0;
-    Ray ray;
-    V3 T = mk(1.f, 1.f, 1.f);
-    uint32_t depth = 0;
-    for (;;) {
-      if (fresh) {  // lib.rs:83-86 + camera.rs:66-74
-        if (s == a.spp) break;
-        rng = splitmix64(hp ^ (uint64_t)s);
-        const float u = ((float)i + gen_f32(rng)) / inv_w;
-        const float v = ((float)j + gen_f32(rng)) / inv_h;
-        const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
-        const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
-        ray.o = add(ld3(C.origin), off);
-        ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)),
-                        ld3(C.origin)),
-                    off);
-        ray.time = gen_range(rng, C.time0, C.time1);
-        T = mk(1.f, 1.f, 1.f);
-        depth = a.max_depth;
-        fresh = false;
-        if (depth == 0) { ++s; fresh = true; continue; }
-      }
-      ++nrays;
-      const Best b = trace<COUNT>(S, ray, stk, cnt);
-      bool done = false;
-      V3 L = mk(0.f, 0.f, 0.f);
-      if (b.prim < 0) {  // lib.rs:102-105
-        L = mul(T, bg);
-        done = true;
-      } else {
-        const Rec h = hit_record(S, ray, b);
-        const DevMat& m = S.mats[h.mat];
-        if (m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
-          L = mul(T, tex_value(S, m.tex, h.u, h.v, h.p));
-          done = true;
-        } else if (m.type == MT_LAMBERT) {  // material.rs:42-56
-          V3 dir = add(h.n, unit(rand_in_unit_sphere(rng)));
-          if (near_zero(dir)) dir = h.n;
-          T = mul(T, tex_value(S, m.tex, h.u, h.v, h.p));
-          ray.o = h.p;
-          ray.d = dir;
-        } else if (m.type == MT_METAL) {  // material.rs:78-95
-          V3 refl = reflect(unit(ray.d), h.n);
-          V3 dir = add(refl, scale(rand_in_unit_sphere(rng), m.param));
-          if (dot(dir, h.n) > 0.0f) {
-            T = mul(T, ld3(m.albedo));
-            ray.o = h.p;
-            ray.d = dir;
-          } else {
-            done = true;  // absorbed: emitted() is black
-          }
-        } else {  // Dielectric, material.rs:116-142
-          const float ratio = h.front ? 1.0f / m.param : m.param;
-          const V3 ud = unit(ray.d);
-          const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
-          const float sin_t = sqrtf(1.0f - cos_t * cos_t);
-          const bool cannot = (ratio * sin_t) > 1.0f;
-          V3 dir;
-          if (cannot || reflectance(cos_t, ratio) > gen_f32(rng)) dir = reflect(ud, h.n);
-          else dir = refract(ud, h.n, ratio);
-          ray.o = h.p;
-          ray.d = dir;  // attenuation (1,1,1): T unchanged
+  uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
+  bool exhausted = false;                // wave-uniform
+  bool has = false;
+  PathState st;
+  st.pid = 0;
+  st.rng = 0;
+  st.depth = 0;
+  for (;;) {
+    // ---- regeneration: compact new path ids into the idle lanes
+    const uint64_t need = __ballot(!has);
+    if (need != 0 && !exhausted) {
+      const uint32_t n_need = (uint32_t)__popcll(need);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      const uint64_t avail = pool_end - pool_next;
+      uint64_t nb = P, ne = P;
+      if (avail < n_need) {  // refill: one atomic per BATCH paths
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(a.queue, (unsigned long long)BATCH);
+        b = __shfl(b, 0, 64);
+        if (b < P) {
+          nb = b;
+          ne = b + BATCH < P ? b + BATCH : P;
+        } else {
+          exhausted = true;
         }
-        if (!done && --depth == 0) done = true;  // lib.rs:98-100
       }
-      if (done) {
-        sum = add(sum, L);
-        ++s;
-        fresh = true;
+      if (!has) {
+        const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
+        if ((rank < avail || id < ne) && start_path(a, id, st)) has = true;
+      }
+      if (avail >= n_need) {
+        pool_next += n_need;
+      } else {
+        pool_next = nb + (n_need - avail);
+        pool_end = ne;
+        if (pool_next > pool_end) pool_next = pool_end;
       }
     }
-    float* o = a.tile_ids ? a.out + ((size_t)t_local * 64u + lane) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
-    o[0] = sum.x;
-    o[1] = sum.y;
-    o[2] = sum.z;
+    if (__ballot(has) == 0) {
+      if (exhausted) break;
+      continue;  // every id handed out this round was an off-image pixel: draw again
+    }
+    if (!has) continue;
+    // ---- one segment: closest hit + shading (lib.rs:97-117)
+    ++nrays;
+    const Best b = trace<COUNT>(S, st.ray, stk, cnt);
+    bool done = false;
+    V3 L = mk(0.f, 0.f, 0.f);
+    if (b.prim < 0) {  // lib.rs:102-105
+      L = mul(st.T, bg);
+      done = true;
+    } else {
+      const Rec h = hit_record(S, st.ray, b);
+      const DevMat& m = S.mats[h.mat];
+      if (m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
+        L = mul(st.T, tex_value(S, m.tex, h.u, h.v, h.p));
+        done = true;
+      } else if (m.type == MT_LAMBERT) {  // material.rs:42-56
+        V3 dir = add(h.n, unit(rand_in_unit_sphere(st.rng)));
+        if (near_zero(dir)) dir = h.n;
+        st.T = mul(st.T, tex_value(S, m.tex, h.u, h.v, h.p));
+        st.ray.o = h.p;
+        st.ray.d = dir;
+      } else if (m.type == MT_METAL) {  // material.rs:78-95
+        V3 refl = reflect(unit(st.ray.d), h.n);
+        V3 dir = add(refl, scale(rand_in_unit_sphere(st.rng), m.param));
+        if (dot(dir, h.n) > 0.0f) {
+          st.T = mul(st.T, ld3(m.albedo));
+          st.ray.o = h.p;
+          st.ray.d = dir;
+        } else {
+          done = true;  // absorbed: emitted() is black
+        }
+      } else {  // Dielectric, material.rs:116-142
+        const float ratio = h.front ? 1.0f / m.param : m.param;
+        const V3 ud = unit(st.ray.d);
+        const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
+        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        const bool cannot = (ratio * sin_t) > 1.0f;
+        V3 dir;
+        if (cannot || reflectance(cos_t, ratio) > gen_f32(st.rng)) dir = reflect(ud, h.n);
+        else dir = refract(ud, h.n, ratio);
+        st.ray.o = h.p;
+        st.ray.d = dir;  // attenuation (1,1,1): T unchanged
+      }
+      if (!done && --st.depth == 0) done = true;  // lib.rs:98-100: depth 0 returns black
+    }
+    if (done) {
+      a.sbuf[st.pid] = L.x;
+      a.sbuf[P + st.pid] = L.y;
+      a.sbuf[2 * P + st.pid] = L.z;
+      has = false;
+    }
   }
-  // one atomic per wave for the ray counter
   unsigned long long tot = nrays;
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
   if (lane == 0 && tot) atomicAdd(a.counters, tot);
@@ -497,6 +545,28 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
       if (lane == 0 && c) atomicAdd(a.counters + 1 + q, c);
     }
   }
+}
+
+// Σ over samples in sample order (lib.rs:83-87), one thread per pixel of the pass.
+__global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_slots) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_slots * 64u) return;
+  const uint32_t slot = g >> 6, l = g & 63u, gslot = a.slot_base + slot;
+  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
+  const uint32_t i = (tile % a.tiles_x) * 8u + (l & 7u), row = (tile / a.tiles_x) * 8u + (l >> 3);
+  if (i >= a.w || row >= a.h) return;
+  const uint64_t P = a.n_paths;
+  float x = 0.f, y = 0.f, z = 0.f;
+  uint64_t idx = (uint64_t)slot * a.spp * 64u + l;
+  for (uint32_t s = 0; s < a.spp; ++s, idx += 64u) {
+    x = x + a.sbuf[idx];
+    y = y + a.sbuf[P + idx];
+    z = z + a.sbuf[2 * P + idx];
+  }
+  float* o = a.tile_ids ? a.out + ((size_t)gslot * 64u + l) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
+  o[0] = x;
+  o[1] = y;
+  o[2] = z;
 }
 
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
@@ -575,6 +645,7 @@ void release(Scene& s) {
     if (hipSetDevice(c.device) != hipSuccess) continue;
     if (c.block) hipFree(c.block);
     if (c.counters) hipFree(c.counters);
+    if (c.sbuf) hipFree(c.sbuf);
   }
   s.dev.clear();
 }
@@ -585,9 +656,23 @@ static DeviceCopy* find_copy(Scene& s, int device) {
   return nullptr;
 }
 
+constexpr uint64_t MAX_PASS_PATHS = 1ull << 30;  // 12.9 GB of ordered samples per pass
+
+static int resident_grid(DeviceCopy& c, bool count) {
+  int& g = c.grid[count ? 1 : 0];
+  if (g > 0) return g;
+  int per_cu = 0, cus = 0;
+  hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::path_kernel<true>, dev::BLOCK, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::path_kernel<false>, dev::BLOCK, 0);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
+  g = per_cu * cus;
+  return g;
+}
+
 static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w,
                   uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
-                  uint32_t n_tiles, float* d_out, hipStream_t stream, uint32_t flags, hipEvent_t ev0,
+                  uint32_t n_slots, float* d_out, hipStream_t stream, uint32_t flags, hipEvent_t ev0,
                   hipEvent_t ev1) {
   if (cam->time0 < sc.flat.time_lo || cam->time1 > sc.flat.time_hi)
     return fail(RTW_EINVAL, "camera shutter [%g, %g) outside the committed motion range [%g, %g]",
@@ -607,7 +692,6 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   memcpy(a.bg, bg, sizeof a.bg);
   a.w = w; a.h = h; a.spp = spp; a.max_depth = max_depth;
   a.tiles_x = (w + 7u) / 8u;
-  a.n_tiles = n_tiles;
   a.tile_ids = d_tiles;
   // the host mirror of dev::splitmix64 (seed pre-hash shared by every pixel)
   uint64_t z = seed + 0x9E3779B97F4A7C15ull;
@@ -616,16 +700,39 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   a.seed_hash = z ^ (z >> 31);
   a.out = d_out;
   a.counters = c.counters;
+  a.queue = c.counters + 15;
   HIPCHK(hipMemsetAsync(c.counters, 0, 16 * sizeof(unsigned long long), stream), "hipMemsetAsync");
-  const uint32_t waves_per_block = dev::BLOCK / 64;
-  dim3 grid((n_tiles + waves_per_block - 1) / waves_per_block), block(dev::BLOCK);
   if (ev0) HIPCHK(hipEventRecord(ev0, stream), "hipEventRecord");
-  if (n_tiles) {
-    if (flags & RTW_FLAG_COUNT_TRAVERSAL)
-      hipLaunchKernelGGL(dev::render_kernel<true>, grid, block, 0, stream, a);
-    else
-      hipLaunchKernelGGL(dev::render_kernel<false>, grid, block, 0, stream, a);
-    HIPCHK(hipGetLastError(), "render_kernel launch");
+  if (n_slots && (spp == 0 || max_depth == 0)) {  // lib.rs:83 loops 0 times / :98 returns black
+    size_t n = d_tiles ? (size_t)n_slots * 64 * 3 : (size_t)w * h * 3;
+    HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
+  } else if (n_slots) {
+    const uint64_t per_slot = 64ull * spp;
+    const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, MAX_PASS_PATHS / per_slot);
+    const uint64_t need = std::min<uint64_t>(n_slots, slots_per_pass) * per_slot;
+    if (need > c.sbuf_paths) {  // grow the ordered sample buffer (first render only)
+      if (c.sbuf) HIPCHK(hipFree(c.sbuf), "hipFree(sample buffer)");
+      c.sbuf = nullptr;
+      c.sbuf_paths = 0;
+      HIPCHK(hipMalloc((void**)&c.sbuf, need * 3 * sizeof(float)), "hipMalloc(sample buffer)");
+      c.sbuf_paths = need;
+    }
+    a.sbuf = c.sbuf;
+    const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
+    const int grid = resident_grid(c, count);
+    for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
+      const uint32_t ns = std::min(slots_per_pass, n_slots - base);
+      a.slot_base = base;
+      a.n_paths = (uint64_t)ns * per_slot;
+      if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
+      if (count)
+        hipLaunchKernelGGL(dev::path_kernel<true>, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
+      else
+        hipLaunchKernelGGL(dev::path_kernel<false>, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
+      HIPCHK(hipGetLastError(), "path_kernel launch");
+      hipLaunchKernelGGL(dev::reduce_kernel, dim3((ns * 64u + 255u) / 256u), dim3(256), 0, stream, a, ns);
+      HIPCHK(hipGetLastError(), "reduce_kernel launch");
+    }
   }
   if (ev1) HIPCHK(hipEventRecord(ev1, stream), "hipEventRecord");
   return RTW_OK;

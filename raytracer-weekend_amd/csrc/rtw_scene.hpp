@@ -68,7 +68,10 @@ struct DeviceCopy {
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
-  unsigned long long* counters = nullptr;  // 16 x u64
+  unsigned long long* counters = nullptr;  // 16 x u64: [0..8] stats, [15] path queue
+  float* sbuf = nullptr;                   // ordered per-sample radiance (3 planes)
+  uint64_t sbuf_paths = 0;
+  int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting)
 };
 
 struct Scene {
