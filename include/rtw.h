@@ -59,6 +59,9 @@ typedef struct {
   uint64_t node_visits;    /* only when RTW_FLAG_COUNT_TRAVERSAL */
   uint64_t prim_tests;     /* only when RTW_FLAG_COUNT_TRAVERSAL */
   uint64_t prim_tests_by_type[6]; /* sphere, moving sphere, rect xy, xz, yz, triangle */
+  /* RTW_FLAG_COUNT_TRAVERSAL: SIMD utilisation, pairs of (wave executions, active lanes) for
+   * the BVH node loop, primitive tests and path segments */
+  uint64_t simd[6];
 } rtw_stats;
 
 enum { RTW_FLAG_COUNT_TRAVERSAL = 1 };

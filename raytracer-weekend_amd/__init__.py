@@ -51,13 +51,15 @@ class rtw_camera(C.Structure):  # include/rtw.h, camera.rs:9-20
 class rtw_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("kernel_ms", C.c_double),
                 ("total_ms", C.c_double), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
-                ("prim_tests_by_type", C.c_uint64 * 6)]
+                ("prim_tests_by_type", C.c_uint64 * 6), ("simd", C.c_uint64 * 6)]
 
     def as_dict(self) -> dict:
         return {"rays": int(self.rays), "paths": int(self.paths), "kernel_ms": float(self.kernel_ms),
                 "total_ms": float(self.total_ms), "node_visits": int(self.node_visits),
                 "prim_tests": int(self.prim_tests),
-                "prim_tests_by_type": [int(x) for x in self.prim_tests_by_type]}
+                "prim_tests_by_type": [int(x) for x in self.prim_tests_by_type],
+                "simd_util": {k: (self.simd[2 * q + 1] / (64.0 * self.simd[2 * q]) if self.simd[2 * q] else None)
+                              for q, k in enumerate(("node_loop", "prim_tests", "segments"))}}
 
 
 _F = C.POINTER(C.c_float)

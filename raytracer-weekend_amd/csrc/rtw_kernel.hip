@@ -32,7 +32,7 @@ namespace dev {
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
-constexpr int STACK = 32;
+constexpr int STACK = 40;  // >= BVH depth (<= 31) + 2: internal + parked-leaf entries
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -175,6 +175,16 @@ __device__ __forceinline__ float cand_tri(const Ray& r, const float* q) {
 
 struct Best { float t; uint32_t key; int32_t prim; };
 
+// COUNT build only: wave-level SIMD utilisation.  Adds 1 to cnt[wave_slot] for the first
+// active lane (one per wave execution) and the wave's active-lane count to cnt[lane_slot].
+__device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane_slot) {
+  const uint64_t m = __ballot(1);
+  if ((uint32_t)__lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) {
+    cnt[wave_slot] += 1;
+    cnt[lane_slot] += (uint32_t)__popcll(m);
+  }
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr,
                                           uint32_t& cur_inst, Ray& lr, Best& b, uint32_t* cnt) {
@@ -205,7 +215,7 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
     else t = cand_rect<2>(lr, q0, k);
   }
-  if (COUNT) { cnt[1]++; cnt[2 + type]++; }
+  if (COUNT) { cnt[1]++; cnt[2 + type]++; simd_tick(cnt, 10, 11); }
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
   if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && meta.y > b.key))) {
     b.t = t;
@@ -239,39 +249,65 @@ __device__ Best trace(const DevScene& S, const Ray& r, int32_t* stk, uint32_t* c
   };
   const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
-  int32_t node = 0;
+  // while-while traversal with postponed leaves (Aila & Laine 2009): phase 1 walks internal
+  // nodes; a lane that reaches a leaf parks it (one pending slot, extra leaves go on the stack as
+  // ~(first << 3 | count)) and keeps walking speculatively until every lane of the wave holds a
+  // leaf or has run dry; phase 2 then tests all parked leaves together, so the primitive tests run
+  // with most lanes active instead of one lane at a time.
+  int32_t node = 0;     // internal node to visit next, -1 = none
+  int32_t leaf = 0;     // pending leaf: first prim
+  int32_t leafn = 0;    //               prim count (0 = none)
   int sp = 0;
   // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
-  for (uint32_t guard = 0; guard < (1u << 22); ++guard) {
-    const float4* N = reinterpret_cast<const float4*>(S.nodes + node);
-    const float4 n0 = N[0], n1 = N[1], n2 = N[2];
-    const int4 nc = *reinterpret_cast<const int4*>(N + 3);
-    if (COUNT) cnt[0]++;
-    const float tmax_c = __builtin_fmaf(b.t, 1.0e-5f, b.t) + 1.0e-5f;
-    float tn0, tn1;
-    bool h0 = slab_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, inv, ood, tmax_c, tn0);
-    bool h1 = nc.y >= 0 && slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1);
-    if (h0 && nc.z) {
-      for (int32_t k = 0; k < nc.z; ++k) test_prim<COUNT>(S, (uint32_t)(nc.x + k), r, cur, lr, b, cnt);
-      h0 = false;
+  for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
+    for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
+      if (node < 0 && sp > 0) {  // refill from the stack
+        const int32_t top = stk[(sp - 1) * BLOCK];
+        if (top >= 0) {
+          node = top;
+          --sp;
+        } else if (leafn == 0) {
+          const uint32_t v = ~(uint32_t)top;
+          leaf = (int32_t)(v >> 3);
+          leafn = (int32_t)(v & 7u);
+          --sp;
+        }
+      }
+      if (!__any(node >= 0 && leafn == 0)) break;
+      if (node >= 0) {
+        const float4* N = reinterpret_cast<const float4*>(S.nodes + node);
+        const float4 n0 = N[0], n1 = N[1], n2 = N[2];
+        const int4 nc = *reinterpret_cast<const int4*>(N + 3);
+        if (COUNT) { cnt[0]++; simd_tick(cnt, 8, 9); }
+        const float tmax_c = __builtin_fmaf(b.t, 1.0e-5f, b.t) + 1.0e-5f;
+        float tn0, tn1;
+        const bool h0 = slab_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, inv, ood, tmax_c, tn0);
+        const bool h1 = nc.y >= 0 && slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1);
+        bool in0 = false, in1 = false;
+        if (h0) {
+          if (nc.z == 0) in0 = true;
+          else if (leafn == 0) { leaf = nc.x; leafn = nc.z; }
+          else if (sp < STACK) stk[(sp++) * BLOCK] = (int32_t)~(((uint32_t)nc.x << 3) | (uint32_t)nc.z);
+        }
+        if (h1) {
+          if (nc.w == 0) in1 = true;
+          else if (leafn == 0) { leaf = nc.y; leafn = nc.w; }
+          else if (sp < STACK) stk[(sp++) * BLOCK] = (int32_t)~(((uint32_t)nc.y << 3) | (uint32_t)nc.w);
+        }
+        if (in0 && in1) {
+          const bool first0 = tn0 <= tn1;
+          if (sp < STACK) stk[(sp++) * BLOCK] = first0 ? nc.y : nc.x;
+          node = first0 ? nc.x : nc.y;
+        } else {
+          node = in0 ? nc.x : (in1 ? nc.y : -1);
+        }
+      }
     }
-    if (h1 && nc.w) {
-      for (int32_t k = 0; k < nc.w; ++k) test_prim<COUNT>(S, (uint32_t)(nc.y + k), r, cur, lr, b, cnt);
-      h1 = false;
+    if (leafn > 0) {  // phase 2
+      for (int32_t k = 0; k < leafn; ++k) test_prim<COUNT>(S, (uint32_t)(leaf + k), r, cur, lr, b, cnt);
+      leafn = 0;
     }
-    if (h0 && h1) {
-      const bool first0 = tn0 <= tn1;
-      if (sp < STACK) stk[(sp++) * BLOCK] = first0 ? nc.y : nc.x;  // depth <= 31: never dropped
-      node = first0 ? nc.x : nc.y;
-    } else if (h0) {
-      node = nc.x;
-    } else if (h1) {
-      node = nc.y;
-    } else {
-      if (sp == 0) break;
-      --sp;
-      node = stk[sp * BLOCK];
-    }
+    if (__all(node < 0 && sp == 0)) break;
   }
   return b;
 }
@@ -438,7 +474,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
   const uint64_t P = a.n_paths;
-  uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
   uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
   bool exhausted = false;                // wave-uniform
@@ -486,6 +522,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
     if (!has) continue;
     // ---- one segment: closest hit + shading (lib.rs:97-117)
     ++nrays;
+    if (COUNT) simd_tick(cnt, 12, 13);
     const Best b = trace<COUNT>(S, st.ray, stk, cnt);
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
@@ -539,7 +576,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
   if (lane == 0 && tot) atomicAdd(a.counters, tot);
   if (COUNT) {
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < 14; ++q) {
       unsigned long long c = cnt[q];
       for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
       if (lane == 0 && c) atomicAdd(a.counters + 1 + q, c);
@@ -751,6 +788,7 @@ static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEven
   st->node_visits = cnt[1];
   st->prim_tests = cnt[2];
   for (int k = 0; k < 6; ++k) st->prim_tests_by_type[k] = cnt[3 + k];
+  for (int k = 0; k < 6; ++k) st->simd[k] = cnt[9 + k];
   return RTW_OK;
 }
 
