@@ -19,6 +19,7 @@
 // next sample in the same iteration, so lanes stay busy across paths of 1..50 bounces.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -236,80 +237,100 @@ __device__ __forceinline__ bool slab_test(float lx, float ly, float lz, float hx
   return tn <= tf;
 }
 
+// Resumable closest-hit query.  A traversal can be suspended between two leaf phases and
+// resumed in a later iteration of the path loop, so a wave does not wait for its slowest ray:
+// trace_run returns as soon as `quota` lanes are done and the rest continue next time.
+struct TraceState {
+  Best b;
+  int32_t node;   // internal node to visit next, -1 = none
+  int32_t leaf;   // pending (parked) leaf: first prim
+  int32_t leafn;  //                        prim count (0 = none)
+  int32_t sp;     // LDS stack depth
+  bool on;        // a traversal is in progress
+};
+
 template <bool COUNT>
-__device__ Best trace(const DevScene& S, const Ray& r, int32_t* stk, uint32_t* cnt) {
-  Best b{INFINITY, 0u, -1};
+__device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt) {
+  ts.b = Best{INFINITY, 0u, -1};
   uint32_t cur = 0;
   Ray lr = r;
-  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT>(S, S.always[k], r, cur, lr, b, cnt);
-  if (S.n_nodes == 0) return b;
+  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT>(S, S.always[k], r, cur, lr, ts.b, cnt);
+  ts.node = S.n_nodes ? 0 : -1;
+  ts.leaf = 0;
+  ts.leafn = 0;
+  ts.sp = 0;
+  ts.on = true;
+}
+
+// while-while traversal with postponed leaves (Aila & Laine 2009): phase 1 walks internal nodes;
+// a lane that reaches a leaf parks it (one pending slot, extra leaves go on the stack as
+// ~(first << 3 | count)) and keeps walking speculatively until every lane of the wave holds a
+// leaf or has run dry; phase 2 then tests all parked leaves together, so the primitive tests run
+// with most lanes active instead of one lane at a time.
+template <bool COUNT>
+__device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, uint32_t* cnt,
+                          uint32_t quota) {
   auto safe_inv = [](float d) {
     float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
     return __builtin_amdgcn_rcpf(dd);
   };
   const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
-  // while-while traversal with postponed leaves (Aila & Laine 2009): phase 1 walks internal
-  // nodes; a lane that reaches a leaf parks it (one pending slot, extra leaves go on the stack as
-  // ~(first << 3 | count)) and keeps walking speculatively until every lane of the wave holds a
-  // leaf or has run dry; phase 2 then tests all parked leaves together, so the primitive tests run
-  // with most lanes active instead of one lane at a time.
-  int32_t node = 0;     // internal node to visit next, -1 = none
-  int32_t leaf = 0;     // pending leaf: first prim
-  int32_t leafn = 0;    //               prim count (0 = none)
-  int sp = 0;
+  uint32_t cur = 0;
+  Ray lr = r;
   // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
   for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
     for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
-      if (node < 0 && sp > 0) {  // refill from the stack
-        const int32_t top = stk[(sp - 1) * BLOCK];
-        if (top >= 0) {
-          node = top;
-          --sp;
-        } else if (leafn == 0) {
-          const uint32_t v = ~(uint32_t)top;
-          leaf = (int32_t)(v >> 3);
-          leafn = (int32_t)(v & 7u);
-          --sp;
-        }
+      {  // refill from the stack: an internal node, or a parked leaf if the slot is free
+        const bool can = ts.node < 0 && ts.sp > 0;
+        const int32_t top = can ? stk[(ts.sp - 1) * BLOCK] : 0;
+        const bool popn = can && top >= 0;
+        const bool popl = can && top < 0 && ts.leafn == 0;
+        const uint32_t v = ~(uint32_t)top;
+        ts.node = popn ? top : ts.node;
+        ts.leaf = popl ? (int32_t)(v >> 3) : ts.leaf;
+        ts.leafn = popl ? (int32_t)(v & 7u) : ts.leafn;
+        ts.sp -= (popn || popl) ? 1 : 0;
       }
-      if (!__any(node >= 0 && leafn == 0)) break;
-      if (node >= 0) {
-        const float4* N = reinterpret_cast<const float4*>(S.nodes + node);
+      if (!__any(ts.node >= 0 && ts.leafn == 0)) break;
+      if (ts.node >= 0) {
+        const float4* N = reinterpret_cast<const float4*>(S.nodes + ts.node);
         const float4 n0 = N[0], n1 = N[1], n2 = N[2];
         const int4 nc = *reinterpret_cast<const int4*>(N + 3);
         if (COUNT) { cnt[0]++; simd_tick(cnt, 8, 9); }
-        const float tmax_c = __builtin_fmaf(b.t, 1.0e-5f, b.t) + 1.0e-5f;
+        const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
         float tn0, tn1;
         const bool h0 = slab_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, inv, ood, tmax_c, tn0);
-        const bool h1 = nc.y >= 0 && slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1);
-        bool in0 = false, in1 = false;
-        if (h0) {
-          if (nc.z == 0) in0 = true;
-          else if (leafn == 0) { leaf = nc.x; leafn = nc.z; }
-          else if (sp < STACK) stk[(sp++) * BLOCK] = (int32_t)~(((uint32_t)nc.x << 3) | (uint32_t)nc.z);
-        }
-        if (h1) {
-          if (nc.w == 0) in1 = true;
-          else if (leafn == 0) { leaf = nc.y; leafn = nc.w; }
-          else if (sp < STACK) stk[(sp++) * BLOCK] = (int32_t)~(((uint32_t)nc.y << 3) | (uint32_t)nc.w);
-        }
-        if (in0 && in1) {
-          const bool first0 = tn0 <= tn1;
-          if (sp < STACK) stk[(sp++) * BLOCK] = first0 ? nc.y : nc.x;
-          node = first0 ? nc.x : nc.y;
-        } else {
-          node = in0 ? nc.x : (in1 ? nc.y : -1);
-        }
+        const bool h1 = slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1) && nc.y >= 0;
+        // branch-free child bookkeeping: at most two stack pushes per visit
+        const bool l0 = h0 && nc.z != 0, l1 = h1 && nc.w != 0;  // leaf children hit
+        const bool i0 = h0 && nc.z == 0, i1 = h1 && nc.w == 0;  // internal children hit
+        const bool take0 = l0 && ts.leafn == 0;
+        const bool take1 = l1 && ts.leafn == 0 && !l0;
+        const bool pl0 = l0 && !take0, pl1 = l1 && !take1;
+        const bool both = i0 && i1, near0 = tn0 <= tn1;
+        const int32_t w0 = (int32_t)~(((uint32_t)nc.x << 3) | (uint32_t)nc.z);
+        const int32_t w1 = (int32_t)~(((uint32_t)nc.y << 3) | (uint32_t)nc.w);
+        const int32_t far = near0 ? nc.y : nc.x;
+        const int32_t q0 = pl0 ? w0 : (pl1 ? w1 : far);
+        const int32_t q1 = (pl0 && pl1) ? w1 : far;
+        const int32_t n = (int32_t)pl0 + (int32_t)pl1 + (int32_t)both;
+        ts.leaf = take0 ? nc.x : (take1 ? nc.y : ts.leaf);
+        ts.leafn = take0 ? nc.z : (take1 ? nc.w : ts.leafn);
+        const int32_t sp = ts.sp;
+        if (n >= 1 && sp < STACK) stk[sp * BLOCK] = q0;
+        if (n >= 2 && sp + 1 < STACK) stk[(sp + 1) * BLOCK] = q1;
+        ts.sp = sp + n;
+        ts.node = both ? (near0 ? nc.x : nc.y) : (i0 ? nc.x : (i1 ? nc.y : -1));
       }
     }
-    if (leafn > 0) {  // phase 2
-      for (int32_t k = 0; k < leafn; ++k) test_prim<COUNT>(S, (uint32_t)(leaf + k), r, cur, lr, b, cnt);
-      leafn = 0;
+    if (ts.leafn > 0) {  // phase 2
+      for (int32_t k = 0; k < ts.leafn; ++k) test_prim<COUNT>(S, (uint32_t)(ts.leaf + k), r, cur, lr, ts.b, cnt);
+      ts.leafn = 0;
     }
-    if (__all(node < 0 && sp == 0)) break;
+    const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
+    if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) break;
   }
-  return b;
 }
 
 // ---- hit record of the winner (hittable/mod.rs:32-48 at every level)
@@ -479,6 +500,8 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
   uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
   bool exhausted = false;                // wave-uniform
   bool has = false;
+  TraceState ts;
+  ts.on = false;
   PathState st;
   st.pid = 0;
   st.rng = 0;
@@ -520,10 +543,19 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
       continue;  // every id handed out this round was an off-image pixel: draw again
     }
     if (!has) continue;
-    // ---- one segment: closest hit + shading (lib.rs:97-117)
-    ++nrays;
+    // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
+    if (!ts.on) {
+      ++nrays;
+      trace_begin<COUNT>(S, st.ray, ts, cnt);
+    }
+    {
+      const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
+      trace_run<COUNT>(S, st.ray, ts, stk, cnt, quota);
+    }
+    if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
+    ts.on = false;
     if (COUNT) simd_tick(cnt, 12, 13);
-    const Best b = trace<COUNT>(S, st.ray, stk, cnt);
+    const Best b = ts.b;
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
     if (b.prim < 0) {  // lib.rs:102-105
@@ -730,6 +762,8 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   a.w = w; a.h = h; a.spp = spp; a.max_depth = max_depth;
   a.tiles_x = (w + 7u) / 8u;
   a.tile_ids = d_tiles;
+  a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
+  if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
   // the host mirror of dev::splitmix64 (seed pre-hash shared by every pixel)
   uint64_t z = seed + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
