@@ -75,6 +75,26 @@ struct alignas(16) DevTex {
   uint32_t off, w, h, pad2;  // texels[off .. off + 3*w*h)
 };
 
+// Scene features: the path kernel is instantiated per feature set so a scene only pays (in code
+// size and register pressure) for the primitive / wrapper / material / texture kinds it uses.
+enum Feature : uint32_t {
+  F_SPHERE = 1u << 0,
+  F_MSPHERE = 1u << 1,
+  F_RECT = 1u << 2,
+  F_TRI = 1u << 3,
+  F_INST = 1u << 4,     // Translation / YRotation wrappers
+  F_UV = 1u << 5,       // a sphere material reads uv (acos / atan2)
+  F_IMAGE = 1u << 6,
+  F_CHECKER = 1u << 7,
+  F_UVDEBUG = 1u << 8,
+  F_LAMBERT = 1u << 9,
+  F_METAL = 1u << 10,
+  F_DIEL = 1u << 11,
+  F_LIGHT = 1u << 12,
+};
+constexpr uint32_t F_ALL = (1u << 13) - 1;
+constexpr uint32_t F_SPHERES = F_SPHERE | F_MSPHERE | F_CHECKER | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
+
 struct DevScene {
   const DevNode* nodes;
   const DevPrim* prims;

@@ -424,6 +424,19 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // feature set (selects the specialised kernel)
+  uint32_t F = 0;
+  for (const DevPrim& p : f.prims) {
+    const uint32_t t = p.type_inst & 0xffu;
+    F |= t == PT_SPHERE ? F_SPHERE : t == PT_MSPHERE ? F_MSPHERE : t == PT_TRI ? F_TRI : F_RECT;
+    if (p.type_inst >> 8) F |= F_INST;
+    if ((t == PT_SPHERE || t == PT_MSPHERE) && f.mats[p.mat].needs_uv) F |= F_UV;
+  }
+  for (const DevMat& m : f.mats)
+    F |= m.type == MT_LAMBERT ? F_LAMBERT : m.type == MT_METAL ? F_METAL : m.type == MT_DIELECTRIC ? F_DIEL : F_LIGHT;
+  for (const DevTex& t : f.texs)
+    F |= t.type == TT_CHECKER ? F_CHECKER : t.type == TT_IMAGE ? F_IMAGE : t.type == TT_UVDEBUG ? F_UVDEBUG : 0u;
+  f.features = F;
   // structural self-check: every internal node reached exactly once from the root, every
   // leaf range inside the BVH part of prims[], every BVH prim covered exactly once
   if (!f.nodes.empty()) {

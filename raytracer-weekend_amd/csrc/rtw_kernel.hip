@@ -33,7 +33,8 @@ namespace dev {
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
-constexpr int STACK = 40;  // >= BVH depth (<= 31) + 2: internal + parked-leaf entries
+constexpr int STACK_DEEP = 40;     // >= BVH depth (<= 31) + 2: internal + parked-leaf entries
+constexpr int STACK_SHALLOW = 16;  // scenes whose BVH depth is <= 14 (jumpy-balls: 10, cornell: 6)
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -186,35 +187,34 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
   }
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr,
-                                          uint32_t& cur_inst, Ray& lr, Best& b, uint32_t* cnt) {
+template <bool COUNT, uint32_t FEAT>
+__device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
+                                          uint32_t* cnt) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
   const float4 q0v = P[0];
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
-  if (inst != cur_inst) {
-    cur_inst = inst;
-    lr = inst ? to_local(S.insts + inst, wr) : wr;
-  }
+  // object-space ray of the prim's wrapper chain; recomputed per test (a few flops) rather than
+  // cached, which keeps 8 VGPRs free for occupancy
+  const Ray lr = ((FEAT & F_INST) && inst) ? to_local(S.insts + inst, wr) : wr;
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
-  float t;
-  if (type == PT_SPHERE) {
+  float t = -1.0f;
+  if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
     t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3]);
-  } else if (type == PT_MSPHERE) {
+  } else if ((FEAT & F_MSPHERE) && type == PT_MSPHERE) {
     const float4 q1v = P[1];
     const float q1[4] = {q1v.x, q1v.y, q1v.z, q1v.w};
     const float rad = P[2].x;
     t = cand_sphere(lr, center_at(q0, q1, lr.time), rad);
-  } else if (type == PT_TRI) {
+  } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float4 q1v = P[1], q2v = P[2];
     const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
     t = cand_tri(lr, q);
-  } else {
+  } else if (FEAT & F_RECT) {
     const float k = P[1].x;
     if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
     else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
-    else t = cand_rect<2>(lr, q0, k);
+    else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
   }
   if (COUNT) { cnt[1]++; cnt[2 + type]++; simd_tick(cnt, 10, 11); }
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
@@ -249,12 +249,10 @@ struct TraceState {
   bool on;        // a traversal is in progress
 };
 
-template <bool COUNT>
+template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt) {
   ts.b = Best{INFINITY, 0u, -1};
-  uint32_t cur = 0;
-  Ray lr = r;
-  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT>(S, S.always[k], r, cur, lr, ts.b, cnt);
+  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt);
   ts.node = S.n_nodes ? 0 : -1;
   ts.leaf = 0;
   ts.leafn = 0;
@@ -267,7 +265,7 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // ~(first << 3 | count)) and keeps walking speculatively until every lane of the wave holds a
 // leaf or has run dry; phase 2 then tests all parked leaves together, so the primitive tests run
 // with most lanes active instead of one lane at a time.
-template <bool COUNT>
+template <bool COUNT, int STACK, uint32_t FEAT>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, uint32_t* cnt,
                           uint32_t quota) {
   auto safe_inv = [](float d) {
@@ -276,8 +274,6 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   };
   const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
-  uint32_t cur = 0;
-  Ray lr = r;
   // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
   for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
     for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
@@ -325,7 +321,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       }
     }
     if (ts.leafn > 0) {  // phase 2
-      for (int32_t k = 0; k < ts.leafn; ++k) test_prim<COUNT>(S, (uint32_t)(ts.leaf + k), r, cur, lr, ts.b, cnt);
+      for (int32_t k = 0; k < ts.leafn; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(ts.leaf + k), r, ts.b, cnt);
       ts.leafn = 0;
     }
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
@@ -347,11 +343,12 @@ __device__ __forceinline__ void sphere_uv(V3 p, float& u, float& v) {  // spheri
   v = theta / PI;
 }
 
+template <uint32_t FEAT>
 __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
   const DevPrim P = S.prims[b.prim];
   const uint32_t type = P.type_inst & 0xffu, inst = P.type_inst >> 8;
   const DevInst* I = S.insts + inst;
-  const Ray lr = inst ? to_local(I, wr) : wr;
+  const Ray lr = ((FEAT & F_INST) && inst) ? to_local(I, wr) : wr;
   const float t = b.t;
   Rec h;
   h.mat = P.mat;
@@ -359,12 +356,12 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
   h.v = 0.0f;
   V3 outward;
   h.p = add(lr.o, scale(lr.d, t));  // ray.rs:25-27
-  if (type == PT_SPHERE || type == PT_MSPHERE) {
+  if (((FEAT & F_SPHERE) && type == PT_SPHERE) || ((FEAT & F_MSPHERE) && type == PT_MSPHERE)) {
     V3 c = type == PT_SPHERE ? ld3(P.q0) : center_at(P.q0, P.q1, lr.time);
     float rad = type == PT_SPHERE ? P.q0[3] : P.q2[0];
     outward = divs(sub(h.p, c), rad);
-    if (S.mats[P.mat].needs_uv) sphere_uv(outward, h.u, h.v);
-  } else if (type == PT_TRI) {
+    if ((FEAT & F_UV) && S.mats[P.mat].needs_uv) sphere_uv(outward, h.u, h.v);
+  } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
                          P.q1[2], P.q1[3], P.q2[0], P.q2[1], P.q2[2], P.q2[3]};
     TriUV s = tri_solve(lr, q);
@@ -382,7 +379,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
     outward = axis == 0 ? mk(0.f, 0.f, 1.f) : (axis == 1 ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f));
   }
   face(h, lr.d, outward);
-  if (inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
+  if ((FEAT & F_INST) && inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
     for (int k = (int)I->nops - 1; k >= 0; --k) {
       V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
       for (int q = 0; q <= k; ++q) {
@@ -406,16 +403,17 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
 }
 
 // ---- textures (texture.rs:56-81, :97-104; image_texture.rs:34-52)
+template <uint32_t FEAT>
 __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) {
   for (int guard = 0; guard < 64; ++guard) {
     const DevTex& t = S.texs[id];
     if (t.type == TT_SOLID) return ld3(t.c);
-    if (t.type == TT_CHECKER) {
+    if ((FEAT & F_CHECKER) && t.type == TT_CHECKER) {
       float sines = sinf(t.freq * p.x) * sinf(t.freq * p.y) * sinf(t.freq * p.z);
       id = sines < 0.0f ? t.odd : t.even;
       continue;
     }
-    if (t.type == TT_IMAGE) {
+    if ((FEAT & F_IMAGE) && t.type == TT_IMAGE) {
       float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
       float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
       float vv = 1.0f - vc;
@@ -428,7 +426,8 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
       const float sc = 1.0f / 255.0f;
       return mk((float)px[0] * sc, (float)px[1] * sc, (float)px[2] * sc);
     }
-    return mk(u, v, 0.0f);  // UVDebug
+    if (FEAT & F_UVDEBUG) return mk(u, v, 0.0f);  // UVDebug
+    break;
   }
   return mk(0.f, 0.f, 0.f);
 }
@@ -487,8 +486,8 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   return true;
 }
 
-template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
+template <bool COUNT, int STACK, int OCC, uint32_t FEAT>
+__global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   __shared__ int32_t stk_all[STACK * BLOCK];
   int32_t* stk = stk_all + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
@@ -546,11 +545,11 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
     if (!ts.on) {
       ++nrays;
-      trace_begin<COUNT>(S, st.ray, ts, cnt);
+      trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt);
     }
     {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
-      trace_run<COUNT>(S, st.ray, ts, stk, cnt, quota);
+      trace_run<COUNT, STACK, FEAT>(S, st.ray, ts, stk, cnt, quota);
     }
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
     ts.on = false;
@@ -562,18 +561,18 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
       L = mul(st.T, bg);
       done = true;
     } else {
-      const Rec h = hit_record(S, st.ray, b);
+      const Rec h = hit_record<FEAT>(S, st.ray, b);
       const DevMat& m = S.mats[h.mat];
-      if (m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
-        L = mul(st.T, tex_value(S, m.tex, h.u, h.v, h.p));
+      if ((FEAT & F_LIGHT) && m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
+        L = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
         done = true;
-      } else if (m.type == MT_LAMBERT) {  // material.rs:42-56
+      } else if ((FEAT & F_LAMBERT) && m.type == MT_LAMBERT) {  // material.rs:42-56
         V3 dir = add(h.n, unit(rand_in_unit_sphere(st.rng)));
         if (near_zero(dir)) dir = h.n;
-        st.T = mul(st.T, tex_value(S, m.tex, h.u, h.v, h.p));
+        st.T = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
         st.ray.o = h.p;
         st.ray.d = dir;
-      } else if (m.type == MT_METAL) {  // material.rs:78-95
+      } else if ((FEAT & F_METAL) && m.type == MT_METAL) {  // material.rs:78-95
         V3 refl = reflect(unit(st.ray.d), h.n);
         V3 dir = add(refl, scale(rand_in_unit_sphere(st.rng), m.param));
         if (dot(dir, h.n) > 0.0f) {
@@ -583,7 +582,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(RenderArgs a) {
         } else {
           done = true;  // absorbed: emitted() is black
         }
-      } else {  // Dielectric, material.rs:116-142
+      } else if (FEAT & F_DIEL) {  // Dielectric, material.rs:116-142
         const float ratio = h.front ? 1.0f / m.param : m.param;
         const V3 ud = unit(st.ray.d);
         const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
@@ -727,12 +726,36 @@ static DeviceCopy* find_copy(Scene& s, int device) {
 
 constexpr uint64_t MAX_PASS_PATHS = 1ull << 30;  // 12.9 GB of ordered samples per pass
 
-static int resident_grid(DeviceCopy& c, bool count) {
+// Variants of the path kernel: feature set x LDS stack depth (by the scene's BVH depth) x the waves
+// per SIMD the register allocator must allow.  Sphere-only scenes (jumpy-balls) get the
+// specialised kernel; everything else the generic one.  RTW_OCC=4|6|8 overrides the occupancy
+// target of the specialised kernel (tuning knob).
+typedef void (*path_fn)(RenderArgs);
+static int env_int(const char* k, int dflt) {
+  const char* e = getenv(k);
+  return e ? atoi(e) : dflt;
+}
+template <bool C>
+static path_fn pick_kernel(uint32_t feat, bool shallow) {
+  if ((feat & ~F_SPHERES) == 0 && shallow) {
+    switch (env_int("RTW_OCC", 4)) {
+      case 4: return dev::path_kernel<C, dev::STACK_SHALLOW, 4, F_SPHERES>;
+      case 8: return dev::path_kernel<C, dev::STACK_SHALLOW, 8, F_SPHERES>;
+      default: return dev::path_kernel<C, dev::STACK_SHALLOW, 6, F_SPHERES>;
+    }
+  }
+  if ((feat & ~F_SPHERES) == 0) return dev::path_kernel<C, dev::STACK_DEEP, 4, F_SPHERES>;
+  return shallow ? dev::path_kernel<C, dev::STACK_SHALLOW, 4, F_ALL> : dev::path_kernel<C, dev::STACK_DEEP, 4, F_ALL>;
+}
+static path_fn path_kernel_ptr(bool count, uint32_t feat, bool shallow) {
+  return count ? pick_kernel<true>(feat, shallow) : pick_kernel<false>(feat, shallow);
+}
+
+static int resident_grid(DeviceCopy& c, path_fn fn, bool count) {
   int& g = c.grid[count ? 1 : 0];
   if (g > 0) return g;
   int per_cu = 0, cus = 0;
-  hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::path_kernel<true>, dev::BLOCK, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::path_kernel<false>, dev::BLOCK, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, dev::BLOCK, 0);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
   g = per_cu * cus;
@@ -790,16 +813,15 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const int grid = resident_grid(c, count);
+    const bool shallow = sc.flat.depth + 2 <= (uint32_t)dev::STACK_SHALLOW;
+    const path_fn fn = path_kernel_ptr(count, sc.flat.features, shallow);
+    const int grid = resident_grid(c, fn, count);
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
       a.n_paths = (uint64_t)ns * per_slot;
       if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
-      if (count)
-        hipLaunchKernelGGL(dev::path_kernel<true>, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
-      else
-        hipLaunchKernelGGL(dev::path_kernel<false>, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
       HIPCHK(hipGetLastError(), "path_kernel launch");
       hipLaunchKernelGGL(dev::reduce_kernel, dim3((ns * 64u + 255u) / 256u), dim3(256), 0, stream, a, ns);
       HIPCHK(hipGetLastError(), "reduce_kernel launch");

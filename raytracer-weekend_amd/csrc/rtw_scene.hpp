@@ -60,6 +60,7 @@ struct Flat {
   std::vector<DevTex> texs;
   std::vector<uint8_t> texels;
   uint32_t depth = 0;
+  uint32_t features = 0;  // Feature bits actually used
   float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover
 };
 
@@ -71,7 +72,8 @@ struct DeviceCopy {
   unsigned long long* counters = nullptr;  // 16 x u64: [0..8] stats, [15] path queue
   float* sbuf = nullptr;                   // ordered per-sample radiance (3 planes)
   uint64_t sbuf_paths = 0;
-  int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting)
+  int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting); the
+                                           // variant is fixed per scene (features, depth)
 };
 
 struct Scene {
