@@ -402,6 +402,24 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
   return h;
 }
 
+// Checker::value's decision (texture.rs:69-81) is `sinf(fx) * sinf(fy) * sinf(fz) < 0`.  Only the
+// signs matter when no factor is zero and the product cannot underflow, and sign(sin x) is the
+// parity of floor(x / pi).  oracle/tools/sin_sign_check.c verifies exhaustively that for every
+// float 2^-12 <= |x| < 65536 the double-precision parity equals the sign of libm's sinf and
+// |sinf x| >= 8.4e-9 (so the product of three stays normal): identical decisions, 3 double
+// multiply+floor instead of 3 sinf.  Outside that range the literal expression is evaluated.
+__device__ __forceinline__ bool checker_odd(float fx, float fy, float fz) {
+  const float ax = fabsf(fx), ay = fabsf(fy), az = fabsf(fz);
+  const float lo = 0x1p-12f, hi = 65536.0f;
+  if (ax >= lo && ax < hi && ay >= lo && ay < hi && az >= lo && az < hi) {
+    const double INV_PI = 0.31830988618379067154;
+    const long long k = (long long)floor((double)fx * INV_PI) + (long long)floor((double)fy * INV_PI) +
+                        (long long)floor((double)fz * INV_PI);
+    return (k & 1) != 0;
+  }
+  return sinf(fx) * sinf(fy) * sinf(fz) < 0.0f;
+}
+
 // ---- textures (texture.rs:56-81, :97-104; image_texture.rs:34-52)
 template <uint32_t FEAT>
 __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) {
@@ -409,8 +427,7 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
     const DevTex& t = S.texs[id];
     if (t.type == TT_SOLID) return ld3(t.c);
     if ((FEAT & F_CHECKER) && t.type == TT_CHECKER) {
-      float sines = sinf(t.freq * p.x) * sinf(t.freq * p.y) * sinf(t.freq * p.z);
-      id = sines < 0.0f ? t.odd : t.even;
+      id = checker_odd(t.freq * p.x, t.freq * p.y, t.freq * p.z) ? t.odd : t.even;
       continue;
     }
     if ((FEAT & F_IMAGE) && t.type == TT_IMAGE) {

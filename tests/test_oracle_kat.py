@@ -129,3 +129,22 @@ def test_tonemap_edges(orc):
     assert L.oracle_tonemap(1e9, 10) == 255
     assert L.oracle_tonemap(10.0, 10) == 255  # sqrt(1) clamps to 0.999 -> 255.74 -> 255
     assert L.oracle_tonemap(2.5, 10) == 127  # sqrt(0.25) * 255.999 = 127.99
+
+
+def test_checker_sign_fast_path_sample():
+    """The kernel decides Checker (texture.rs:69-81) by the parity of floor(x/pi) for
+    2^-12 <= |x| < 65536; oracle/tools/sin_sign_check.c proves it exhaustively against libm's
+    sinf.  This re-checks a random sample (plus values next to multiples of pi) on every run."""
+    libm = C.CDLL("libm.so.6")
+    libm.sinf.restype = C.c_float
+    libm.sinf.argtypes = [C.c_float]
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-65536, 65536, 100000),
+                         np.exp(rng.uniform(np.log(2.0 ** -12), np.log(65536.0), 50000)),
+                         np.pi * np.arange(1, 20000)]).astype(np.float32)
+    xs = xs[(np.abs(xs) >= 2.0 ** -12) & (np.abs(xs) < 65536)]
+    nb = np.nextafter(xs, np.float32(np.inf)).astype(np.float32)
+    for arr in (xs, nb):
+        par = np.floor(arr.astype(np.float64) * 0.31830988618379067154).astype(np.int64) & 1
+        sgn = np.array([libm.sinf(float(x)) < 0 for x in arr])
+        assert np.array_equal(par.astype(bool), sgn)
