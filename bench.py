@@ -112,6 +112,10 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default="", help="PMC HBM bytes per launch (from profiles/)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path on one GPU")
+    ap.add_argument("--check-image", action="store_true",
+                    help="rank 0 checks the gathered frame bit-for-bit against a single-device render")
     args = ap.parse_args()
 
     import torch
@@ -122,8 +126,12 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dev_id = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_id)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_id}"))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -167,7 +175,14 @@ def main() -> int:
                 ev[k][1].record(stream)
 
     def frame_end():
-        if world > 1:
+        if world > 1 and args.backend == "gloo":  # CPU rehearsal: gather through host memory
+            g = torch.zeros(gathered.shape, dtype=torch.float32)
+            dist.all_gather_into_tensor(g, packed.cpu())
+            gathered.copy_(g)
+            if rank == 0:
+                rtw.unpack_tiles_device(w, h, all_ids.data_ptr(), world * per_rank, gathered.data_ptr(),
+                                        image.data_ptr(), dev, stream.cuda_stream)
+        elif world > 1:
             dist.all_gather_into_tensor(gathered, packed)
             if rank == 0:
                 rtw.unpack_tiles_device(w, h, all_ids.data_ptr(), world * per_rank, gathered.data_ptr(),
@@ -191,6 +206,18 @@ def main() -> int:
     for _ in range(args.warmup):
         render_frame(False)
         frame_end()
+    if args.check_image:  # the gathered frame must equal a single-device render, bit for bit
+        render_frame(False)
+        frame_end()
+        torch.cuda.synchronize()
+        if rank == 0:
+            ref = torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
+            rt.render_device(ref.data_ptr(), dev, 0, 0, stream.cuda_stream)
+            torch.cuda.synchronize()
+            same = bool(torch.equal(ref.view(torch.int32), image.view(torch.int32)))
+            print(json.dumps({"check_image": same, "world": world}), flush=True)
+            if not same:
+                raise SystemExit("gathered frame differs from the single-device render")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -239,7 +266,7 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded scene generator, scenes.rs restated; seed %d)" % SCENE_SEED,
-            "config": {"workload": cfg_text, "scene": scene_name, "width": w, "height": h, "spp": spp,
+            "config": {"workload": cfg_text, "backend": args.backend if world > 1 else None, "scene": scene_name, "width": w, "height": h, "spp": spp,
                        "max_depth": 50, "rays_per_frame": frame_rays, "paths_per_frame": w * h * spp,
                        "tiles": nt, "launches_per_frame": launches, "parallelism": f"tiles{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
