@@ -247,9 +247,14 @@ def main() -> int:
     alg_bytes_frame = RAY_STATE_B * rays_r + 2 * NODE_BOX_B * nodes_r + prim_bytes
     alg_bytes_rank = alg_bytes_frame / world
     achieved = alg_bytes_rank / (frame_kernel_ms * 1e-3) / 1e9
-    traffic = None
-    if args.traffic_json and Path(args.traffic_json).exists():
-        traffic = json.loads(Path(args.traffic_json).read_text()).get("hbm_bytes_per_launch")
+    # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +
+    # WRITE_SIZE, separate passes; scripts/gpu_profile.sh + scripts/prof_summary.py), if any
+    traffic, traffic_src = None, None
+    tj = Path(args.traffic_json) if args.traffic_json else ROOT / "profiles" / f"pmc_{args.config}.json"
+    if tj.exists() and not args.spp:
+        d = json.loads(tj.read_text())
+        if d.get("launches_per_frame", 1) == launches and d.get("world", 1) == world:
+            traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(ROOT))
 
     out = None
     if rank == 0:
@@ -271,7 +276,7 @@ def main() -> int:
                        "tiles": nt, "launches_per_frame": launches, "parallelism": f"tiles{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "render_kernel<false>",
+                         "traffic_source": traffic_src, "kernel": "path_kernel",
                          "kernel_ms_per_frame": round(frame_kernel_ms, 3),
                          "alg_bytes_per_ray": round(alg_bytes_frame / max(1, frame_rays), 2),
                          "node_fetches_per_ray": round(nodes_r / max(1, rays_r), 3),

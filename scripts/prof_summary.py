@@ -36,9 +36,18 @@ for k, v in out["pmc"].items():
     v["fetch_bytes_per_launch_raw"] = fetch
     v["write_bytes_per_launch"] = write
     v["hbm_bytes_per_launch"] = 2 * fetch + write
-main = [k for k in out["pmc"] if "path_kernel<false>" in k]
+main = [k for k in out["pmc"] if "path_kernel<false" in k]
 if main:
     out["hbm_bytes_per_launch"] = out["pmc"][main[0]]["hbm_bytes_per_launch"]
     out["kernel"] = main[0]
 (dst / "summary.json").write_text(json.dumps(out, indent=1))
+if len(sys.argv) > 4 and main:  # also publish the per-config traffic file bench.py reads
+    cfg = sys.argv[4]
+    pub = {"config": cfg, "world": 1, "launches_per_frame": 1, "kernel": main[0],
+           "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
+           "fetch_bytes_per_launch_raw": out["pmc"][main[0]]["fetch_bytes_per_launch_raw"],
+           "write_bytes_per_launch": out["pmc"][main[0]]["write_bytes_per_launch"],
+           "correction": "FETCH_SIZE x2 (gfx950 counts 64 B per 128-B request), WRITE_SIZE as is; KiB -> B",
+           "source": str(dst)}
+    (dst.parent / f"pmc_{cfg}.json").write_text(json.dumps(pub, indent=1))
 print(json.dumps(out, indent=1))
