@@ -47,7 +47,8 @@ RENDER_SEED = 2024
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # BASELINE.md roofline definition: algorithmic bytes per ray
 RAY_STATE_B = 64
-NODE_BOX_B = 32            # per box tested; one DevNode fetch tests 2 child boxes
+NODE_BOX_B = 32            # per box tested
+BOXES_PER_NODE = 4         # one DevNode4 fetch tests 4 child boxes (BVH4)
 PRIM_B = [16, 36, 20, 20, 20, 36]  # sphere, moving sphere, rect xy/xz/yz, triangle
 
 
@@ -244,7 +245,7 @@ def main() -> int:
     rays_r = counts[0]
     nodes_r = counts[1]
     prim_bytes = float(np.dot(counts[2:8], PRIM_B))
-    alg_bytes_frame = RAY_STATE_B * rays_r + 2 * NODE_BOX_B * nodes_r + prim_bytes
+    alg_bytes_frame = RAY_STATE_B * rays_r + BOXES_PER_NODE * NODE_BOX_B * nodes_r + prim_bytes
     alg_bytes_rank = alg_bytes_frame / world
     achieved = alg_bytes_rank / (frame_kernel_ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +

@@ -418,7 +418,9 @@ int64_t rtw_scene_info(const rtw_scene* s, int what) {
   switch (what) {
     case 1: return (int64_t)sc.mat.size();
     case 2: return (int64_t)sc.tex.size();
-    case 3: return (int64_t)sc.flat.nodes.size();
+    case 3: return (int64_t)sc.flat.nodes4.size();
+    case 7: return (int64_t)sc.flat.nodes.size();
+    case 8: return (int64_t)sc.flat.stack_need;
     case 4: return (int64_t)sc.flat.depth;
     case 5: return (int64_t)sc.flat.always.size();
     case 6: return (int64_t)sc.flat.insts.size();

@@ -47,6 +47,17 @@ struct alignas(16) DevNode {
 };
 static_assert(sizeof(DevNode) == 64, "DevNode must be 64 B");
 
+// 4-wide BVH node used by the kernel (collapsed from the SAH BVH2).  Planes are stored per axis
+// as [lo x4][hi x4] so a lane loads its ray's near and far planes with one dwordx4 each, picking
+// lo or hi by the sign of its direction: no min/max sort in the slab test.  Empty slots have an
+// inverted box (lo = +inf, hi = -inf), which that formulation always misses.
+struct alignas(16) DevNode4 {
+  float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+  int32_t child[4];  // >= 0: node4 index; < 0: leaf word ~(first_prim << 3 | count)
+  uint32_t pad[4];
+};
+static_assert(sizeof(DevNode4) == 128, "DevNode4 must be 128 B");
+
 struct alignas(16) DevTriShade {
   float n[9];   // vertex normals after defaults (triangular.rs:55)
   float uv[6];  // vertex uvs after defaults (triangular.rs:57-66)
@@ -96,7 +107,7 @@ constexpr uint32_t F_ALL = (1u << 13) - 1;
 constexpr uint32_t F_SPHERES = F_SPHERE | F_MSPHERE | F_CHECKER | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
 
 struct DevScene {
-  const DevNode* nodes;
+  const DevNode4* nodes;
   const DevPrim* prims;
   const uint32_t* always;
   const DevTriShade* tshade;

@@ -336,6 +336,75 @@ struct BvhBuild {
   }
 };
 
+// ---------------------------------------------------------------- BVH2 -> BVH4 collapse
+// Each 4-wide node absorbs up to two BVH2 levels: starting from a BVH2 node's two children, the
+// internal child with the largest surface area is repeatedly replaced by its own two children
+// until there are four.  Leaves keep their prim ranges (leaf word ~(first << 3 | count)).
+struct Collapse {
+  const std::vector<DevNode>& n2;
+  std::vector<DevNode4>& out;
+
+  struct C {
+    Box box;
+    int32_t idx;     // BVH2 node (internal) or first prim (leaf)
+    uint32_t count;  // 0 = internal
+  };
+  static C child(const DevNode& n, int k) {
+    C c;
+    for (int a = 0; a < 3; ++a) {
+      c.box.lo[a] = k ? n.b1lo[a] : n.b0lo[a];
+      c.box.hi[a] = k ? n.b1hi[a] : n.b0hi[a];
+    }
+    c.idx = k ? n.c1 : n.c0;
+    c.count = k ? n.n1 : n.n0;
+    return c;
+  }
+  // returns the node4 index; *bound = worst-case stack entries pushed below (and at) this node
+  int32_t build(int32_t root2, uint32_t* bound) {
+    std::vector<C> ch;
+    const DevNode& r = n2[root2];
+    ch.push_back(child(r, 0));
+    if (r.c1 >= 0 || r.n1) ch.push_back(child(r, 1));
+    while (ch.size() < 4) {
+      int best = -1;
+      float area = -1.f;
+      for (size_t k = 0; k < ch.size(); ++k)
+        if (ch[k].count == 0 && ch[k].box.area() > area) { area = ch[k].box.area(); best = (int)k; }
+      if (best < 0) break;
+      const DevNode& m = n2[ch[best].idx];
+      C a = child(m, 0);
+      ch[best] = a;
+      if (m.c1 >= 0 || m.n1) ch.push_back(child(m, 1));
+    }
+    const int32_t id = (int32_t)out.size();
+    DevNode4 nd;
+    memset(&nd, 0, sizeof nd);
+    for (int k = 0; k < 4; ++k) {
+      nd.lo_x[k] = nd.lo_y[k] = nd.lo_z[k] = INFINITY;
+      nd.hi_x[k] = nd.hi_y[k] = nd.hi_z[k] = -INFINITY;
+    }
+    out.push_back(nd);
+    uint32_t below = 0;
+    for (size_t k = 0; k < ch.size(); ++k) {
+      int32_t word;
+      if (ch[k].count) {
+        word = (int32_t)~(((uint32_t)ch[k].idx << 3) | ch[k].count);
+      } else {
+        uint32_t b = 0;
+        word = build(ch[k].idx, &b);
+        below = std::max(below, b);
+      }
+      DevNode4& o = out[id];
+      o.lo_x[k] = ch[k].box.lo[0]; o.hi_x[k] = ch[k].box.hi[0];
+      o.lo_y[k] = ch[k].box.lo[1]; o.hi_y[k] = ch[k].box.hi[1];
+      o.lo_z[k] = ch[k].box.lo[2]; o.hi_z[k] = ch[k].box.hi[2];
+      o.child[k] = word;
+    }
+    *bound = (uint32_t)ch.size() + below;  // a visit pushes at most all its hit children
+    return id;
+  }
+};
+
 bool texture_reads_uv(const Scene& s, uint32_t t, int guard = 0) {
   if (guard > 64) return false;
   const TexH& x = s.tex[t];
@@ -424,6 +493,39 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // 4-wide tree for the kernel
+  if (!f.nodes.empty()) {
+    for (const Leaf& L : rest) (void)L;
+    if (rest.size() >= (1u << 28)) return fail(RTW_EINVAL, "too many BVH primitives for leaf words");
+    Collapse col{f.nodes, f.nodes4};
+    uint32_t bound = 0;
+    col.build(0, &bound);
+    f.stack_need = bound + 1;
+    if (f.stack_need > 48) return fail(RTW_EINVAL, "BVH4 stack bound %u exceeds the kernel's 48", f.stack_need);
+    // self-check: every node4 reached once, every BVH prim covered once
+    std::vector<uint8_t> seen4(f.nodes4.size(), 0), seenp(rest.size(), 0);
+    std::vector<int32_t> todo{0};
+    seen4[0] = 1;
+    while (!todo.empty()) {
+      const DevNode4 nd = f.nodes4[todo.back()];
+      todo.pop_back();
+      for (int k = 0; k < 4; ++k) {
+        if (nd.lo_x[k] > nd.hi_x[k]) continue;  // empty slot
+        const int32_t w = nd.child[k];
+        if (w >= 0) {
+          if ((size_t)w >= f.nodes4.size() || seen4[w]++) return fail(RTW_EINVAL, "BVH4 node cycle/range");
+          todo.push_back(w);
+        } else {
+          const uint32_t v = ~(uint32_t)w, first = v >> 3, cnt = v & 7u;
+          if (!cnt || (size_t)first + cnt > rest.size()) return fail(RTW_EINVAL, "BVH4 leaf out of range");
+          for (uint32_t q = 0; q < cnt; ++q)
+            if (seenp[first + q]++) return fail(RTW_EINVAL, "BVH4 prim referenced twice");
+        }
+      }
+    }
+    for (uint8_t x : seenp)
+      if (!x) return fail(RTW_EINVAL, "BVH4 misses a primitive");
+  }
   // feature set (selects the specialised kernel)
   uint32_t F = 0;
   for (const DevPrim& p : f.prims) {

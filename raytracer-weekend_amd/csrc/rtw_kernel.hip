@@ -33,8 +33,8 @@ namespace dev {
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
-constexpr int STACK_DEEP = 40;     // >= BVH depth (<= 31) + 2: internal + parked-leaf entries
-constexpr int STACK_SHALLOW = 16;  // scenes whose BVH depth is <= 14 (jumpy-balls: 10, cornell: 6)
+constexpr int STACK_DEEP = 48;     // LDS stack entries per lane, chosen by the tree's worst-case
+constexpr int STACK_SHALLOW = 24;  // push bound (Flat::stack_need): jumpy-balls / cornell fit 24
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -242,11 +242,10 @@ __device__ __forceinline__ bool slab_test(float lx, float ly, float lz, float hx
 // trace_run returns as soon as `quota` lanes are done and the rest continue next time.
 struct TraceState {
   Best b;
-  int32_t node;   // internal node to visit next, -1 = none
-  int32_t leaf;   // pending (parked) leaf: first prim
-  int32_t leafn;  //                        prim count (0 = none)
-  int32_t sp;     // LDS stack depth
-  bool on;        // a traversal is in progress
+  int32_t node;  // node4 to visit next, -1 = none
+  int32_t pend;  // parked leaf word ~(first << 3 | count), 0 = none
+  int32_t sp;    // LDS stack depth
+  bool on;       // a traversal is in progress
 };
 
 template <bool COUNT, uint32_t FEAT>
@@ -254,17 +253,15 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
   ts.b = Best{INFINITY, 0u, -1};
   for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt);
   ts.node = S.n_nodes ? 0 : -1;
-  ts.leaf = 0;
-  ts.leafn = 0;
+  ts.pend = 0;
   ts.sp = 0;
   ts.on = true;
 }
 
-// while-while traversal with postponed leaves (Aila & Laine 2009): phase 1 walks internal nodes;
-// a lane that reaches a leaf parks it (one pending slot, extra leaves go on the stack as
-// ~(first << 3 | count)) and keeps walking speculatively until every lane of the wave holds a
-// leaf or has run dry; phase 2 then tests all parked leaves together, so the primitive tests run
-// with most lanes active instead of one lane at a time.
+// while-while walk of the 4-wide BVH with postponed leaves (Aila & Laine 2009): phase 1 visits
+// internal nodes (nearest hit child next, the other hit children pushed); a lane that reaches a
+// leaf parks it (one slot; further leaves go on the stack) and keeps walking speculatively until
+// every lane of the wave holds a leaf or has run dry; phase 2 tests all parked leaves together.
 template <bool COUNT, int STACK, uint32_t FEAT>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, uint32_t* cnt,
                           uint32_t quota) {
@@ -274,6 +271,9 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   };
   const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
+  // near / far plane float offsets inside DevNode4 by the ray's direction signs
+  const int nx = inv.x < 0.f ? 4 : 0, ny = (inv.y < 0.f ? 4 : 0) + 8, nz = (inv.z < 0.f ? 4 : 0) + 16;
+  const int fx = nx ^ 4, fy = ny ^ 4, fz = nz ^ 4;
   // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
   for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
     for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
@@ -281,48 +281,72 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         const bool can = ts.node < 0 && ts.sp > 0;
         const int32_t top = can ? stk[(ts.sp - 1) * BLOCK] : 0;
         const bool popn = can && top >= 0;
-        const bool popl = can && top < 0 && ts.leafn == 0;
-        const uint32_t v = ~(uint32_t)top;
+        const bool popl = can && top < 0 && ts.pend == 0;
         ts.node = popn ? top : ts.node;
-        ts.leaf = popl ? (int32_t)(v >> 3) : ts.leaf;
-        ts.leafn = popl ? (int32_t)(v & 7u) : ts.leafn;
+        ts.pend = popl ? top : ts.pend;
         ts.sp -= (popn || popl) ? 1 : 0;
       }
-      if (!__any(ts.node >= 0 && ts.leafn == 0)) break;
+      if (!__any(ts.node >= 0 && ts.pend == 0)) break;
       if (ts.node >= 0) {
-        const float4* N = reinterpret_cast<const float4*>(S.nodes + ts.node);
-        const float4 n0 = N[0], n1 = N[1], n2 = N[2];
-        const int4 nc = *reinterpret_cast<const int4*>(N + 3);
+        const float* N = reinterpret_cast<const float*>(S.nodes + ts.node);
+        const float4 qnx = *reinterpret_cast<const float4*>(N + nx), qfx = *reinterpret_cast<const float4*>(N + fx);
+        const float4 qny = *reinterpret_cast<const float4*>(N + ny), qfy = *reinterpret_cast<const float4*>(N + fy);
+        const float4 qnz = *reinterpret_cast<const float4*>(N + nz), qfz = *reinterpret_cast<const float4*>(N + fz);
+        const int4 cw = *reinterpret_cast<const int4*>(N + 24);
         if (COUNT) { cnt[0]++; simd_tick(cnt, 8, 9); }
         const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
-        float tn0, tn1;
-        const bool h0 = slab_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, inv, ood, tmax_c, tn0);
-        const bool h1 = slab_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, inv, ood, tmax_c, tn1) && nc.y >= 0;
-        // branch-free child bookkeeping: at most two stack pushes per visit
-        const bool l0 = h0 && nc.z != 0, l1 = h1 && nc.w != 0;  // leaf children hit
-        const bool i0 = h0 && nc.z == 0, i1 = h1 && nc.w == 0;  // internal children hit
-        const bool take0 = l0 && ts.leafn == 0;
-        const bool take1 = l1 && ts.leafn == 0 && !l0;
-        const bool pl0 = l0 && !take0, pl1 = l1 && !take1;
-        const bool both = i0 && i1, near0 = tn0 <= tn1;
-        const int32_t w0 = (int32_t)~(((uint32_t)nc.x << 3) | (uint32_t)nc.z);
-        const int32_t w1 = (int32_t)~(((uint32_t)nc.y << 3) | (uint32_t)nc.w);
-        const int32_t far = near0 ? nc.y : nc.x;
-        const int32_t q0 = pl0 ? w0 : (pl1 ? w1 : far);
-        const int32_t q1 = (pl0 && pl1) ? w1 : far;
-        const int32_t n = (int32_t)pl0 + (int32_t)pl1 + (int32_t)both;
-        ts.leaf = take0 ? nc.x : (take1 ? nc.y : ts.leaf);
-        ts.leafn = take0 ? nc.z : (take1 ? nc.w : ts.leafn);
-        const int32_t sp = ts.sp;
-        if (n >= 1 && sp < STACK) stk[sp * BLOCK] = q0;
-        if (n >= 2 && sp + 1 < STACK) stk[(sp + 1) * BLOCK] = q1;
-        ts.sp = sp + n;
-        ts.node = both ? (near0 ? nc.x : nc.y) : (i0 ? nc.x : (i1 ? nc.y : -1));
+        float tn[4];
+        bool hit[4];
+        const float NX[4] = {qnx.x, qnx.y, qnx.z, qnx.w}, FX[4] = {qfx.x, qfx.y, qfx.z, qfx.w};
+        const float NY[4] = {qny.x, qny.y, qny.z, qny.w}, FY[4] = {qfy.x, qfy.y, qfy.z, qfy.w};
+        const float NZ[4] = {qnz.x, qnz.y, qnz.z, qnz.w}, FZ[4] = {qfz.x, qfz.y, qfz.z, qfz.w};
+        const int32_t CW[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // conservative slab test (culling only)
+          const float a = __builtin_fmaf(NX[k], inv.x, -ood.x), b = __builtin_fmaf(NY[k], inv.y, -ood.y);
+          const float c = __builtin_fmaf(NZ[k], inv.z, -ood.z);
+          const float d = __builtin_fmaf(FX[k], inv.x, -ood.x), e = __builtin_fmaf(FY[k], inv.y, -ood.y);
+          const float f = __builtin_fmaf(FZ[k], inv.z, -ood.z);
+          tn[k] = fmaxf(fmaxf(fmaxf(a, b), c), 0.0f);
+          hit[k] = tn[k] <= fminf(fminf(fminf(d, e), f), tmax_c);
+        }
+        // nearest hit internal child -> next node; the other hit children -> stack / parked slot
+        int32_t next = -1;
+        float best = INFINITY;
+        int bk = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool in = hit[k] && CW[k] >= 0 && tn[k] < best;
+          best = in ? tn[k] : best;
+          bk = in ? k : bk;
+          next = in ? CW[k] : next;
+        }
+        int32_t pend = ts.pend;
+        uint32_t push = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool leaf_take = hit[k] && CW[k] < 0 && pend == 0;
+          pend = leaf_take ? CW[k] : pend;
+          push |= (hit[k] && k != bk && !leaf_take) ? (1u << k) : 0u;
+        }
+        ts.pend = pend;
+        int32_t sp = ts.sp;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if ((push >> k) & 1u) {
+            if (sp < STACK) stk[sp * BLOCK] = CW[k];
+            ++sp;
+          }
+        }
+        ts.sp = sp;
+        ts.node = next;
       }
     }
-    if (ts.leafn > 0) {  // phase 2
-      for (int32_t k = 0; k < ts.leafn; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(ts.leaf + k), r, ts.b, cnt);
-      ts.leafn = 0;
+    if (ts.pend != 0) {  // phase 2
+      const uint32_t v = ~(uint32_t)ts.pend;
+      const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
+      for (int32_t k = 0; k < n; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt);
+      ts.pend = 0;
     }
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
     if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) break;
@@ -691,7 +715,7 @@ int upload(Scene& s, int device) {
   if (device >= ndev) return fail(RTW_EINVAL, "device %d >= device count %d", device, ndev);
   const Flat& f = s.flat;
   std::vector<uint8_t> blob;
-  size_t o_nodes = put(blob, f.nodes), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
+  size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels);
   blob.resize((blob.size() + 255) & ~(size_t)255);
@@ -707,7 +731,7 @@ int upload(Scene& s, int device) {
     HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
     HIPCHK(hipMalloc((void**)&c.counters, 16 * sizeof(unsigned long long)), "hipMalloc(counters)");
     uint8_t* base = (uint8_t*)c.block;
-    c.scene.nodes = (const DevNode*)(base + o_nodes);
+    c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
     c.scene.always = (const uint32_t*)(base + o_always);
     c.scene.tshade = (const DevTriShade*)(base + o_tsh);
@@ -715,7 +739,7 @@ int upload(Scene& s, int device) {
     c.scene.mats = (const DevMat*)(base + o_mat);
     c.scene.texs = (const DevTex*)(base + o_tex);
     c.scene.texels = (const uint8_t*)(base + o_texel);
-    c.scene.n_nodes = (uint32_t)f.nodes.size();
+    c.scene.n_nodes = (uint32_t)f.nodes4.size();
     c.scene.n_prims = (uint32_t)f.prims.size();
     c.scene.n_always = (uint32_t)f.always.size();
     c.scene.n_insts = (uint32_t)f.insts.size();
@@ -830,7 +854,7 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const bool shallow = sc.flat.depth + 2 <= (uint32_t)dev::STACK_SHALLOW;
+    const bool shallow = sc.flat.stack_need <= (uint32_t)dev::STACK_SHALLOW;
     const path_fn fn = path_kernel_ptr(count, sc.flat.features, shallow);
     const int grid = resident_grid(c, fn, count);
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {

@@ -51,7 +51,9 @@ struct MatH {
 
 // Flattened host copy of what goes to every device.
 struct Flat {
-  std::vector<DevNode> nodes;
+  std::vector<DevNode> nodes;    // SAH BVH2 (build + self-check)
+  std::vector<DevNode4> nodes4;  // what the kernel walks
+  uint32_t stack_need = 0;       // worst-case traversal stack entries of nodes4
   std::vector<DevPrim> prims;
   std::vector<uint32_t> always;
   std::vector<DevTriShade> tshade;
