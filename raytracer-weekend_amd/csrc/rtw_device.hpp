@@ -138,6 +138,9 @@ struct RenderArgs {
   float* out;
   unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
   unsigned long long* queue;     // path-id dispenser of this pass
+  int32_t* spill;                // traversal stack entries beyond the LDS stack: [depth][lane]
+  uint32_t spill_depth;          // entries per lane (0 = the LDS stack covers the tree's bound)
+  uint32_t spill_lanes;          // resident lanes of the launch (stride between levels)
 };
 
 }  // namespace rtw

@@ -385,6 +385,7 @@ struct Collapse {
     }
     out.push_back(nd);
     uint32_t below = 0;
+    bool inner = false;
     for (size_t k = 0; k < ch.size(); ++k) {
       int32_t word;
       if (ch[k].count) {
@@ -393,6 +394,7 @@ struct Collapse {
         uint32_t b = 0;
         word = build(ch[k].idx, &b);
         below = std::max(below, b);
+        inner = true;
       }
       DevNode4& o = out[id];
       o.lo_x[k] = ch[k].box.lo[0]; o.hi_x[k] = ch[k].box.hi[0];
@@ -400,7 +402,9 @@ struct Collapse {
       o.lo_z[k] = ch[k].box.lo[2]; o.hi_z[k] = ch[k].box.hi[2];
       o.child[k] = word;
     }
-    *bound = (uint32_t)ch.size() + below;  // a visit pushes at most all its hit children
+    // a visit pushes every hit child except the nearest internal one, which it walks into next
+    // (trace_run); with no internal child it may push them all
+    *bound = inner ? (uint32_t)ch.size() - 1 + below : (uint32_t)ch.size();
     return id;
   }
 };
@@ -495,13 +499,12 @@ int flatten(Scene& s) {
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
   // 4-wide tree for the kernel
   if (!f.nodes.empty()) {
-    for (const Leaf& L : rest) (void)L;
     if (rest.size() >= (1u << 28)) return fail(RTW_EINVAL, "too many BVH primitives for leaf words");
     Collapse col{f.nodes, f.nodes4};
     uint32_t bound = 0;
     col.build(0, &bound);
-    f.stack_need = bound + 1;
-    if (f.stack_need > 48) return fail(RTW_EINVAL, "BVH4 stack bound %u exceeds the kernel's 48", f.stack_need);
+    f.stack_need = bound;  // entries beyond the kernel's LDS stack spill to a per-lane HBM area
+    if (f.stack_need > 4096) return fail(RTW_EINVAL, "BVH4 stack bound %u is unreasonable", f.stack_need);
     // self-check: every node4 reached once, every BVH prim covered once
     std::vector<uint8_t> seen4(f.nodes4.size(), 0), seenp(rest.size(), 0);
     std::vector<int32_t> todo{0};

@@ -33,8 +33,11 @@ namespace dev {
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
-constexpr int STACK_DEEP = 48;     // LDS stack entries per lane, chosen by the tree's worst-case
-constexpr int STACK_SHALLOW = 24;  // push bound (Flat::stack_need): jumpy-balls / cornell fit 24
+// LDS traversal-stack entries per lane.  160 KB of LDS per CU holds 5 blocks of 256 lanes x 32
+// entries, so the stack never limits occupancy below the 4-5 waves/SIMD the registers allow; a tree
+// whose worst-case push bound (Flat::stack_need) is deeper spills the excess to HBM (RenderArgs::spill).
+constexpr int STACK_LDS = 32;
+constexpr int STACK_LDS6 = 24;  // 6 waves/SIMD variant
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -262,9 +265,9 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // internal nodes (nearest hit child next, the other hit children pushed); a lane that reaches a
 // leaf parks it (one slot; further leaves go on the stack) and keeps walking speculatively until
 // every lane of the wave holds a leaf or has run dry; phase 2 tests all parked leaves together.
-template <bool COUNT, int STACK, uint32_t FEAT>
-__device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, uint32_t* cnt,
-                          uint32_t quota) {
+template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT>
+__device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
+                          uint32_t spill_lanes, uint32_t* cnt, uint32_t quota) {
   auto safe_inv = [](float d) {
     float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
     return __builtin_amdgcn_rcpf(dd);
@@ -279,7 +282,11 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
       {  // refill from the stack: an internal node, or a parked leaf if the slot is free
         const bool can = ts.node < 0 && ts.sp > 0;
-        const int32_t top = can ? stk[(ts.sp - 1) * BLOCK] : 0;
+        int32_t top = 0;
+        if (can) {
+          const int32_t i = ts.sp - 1;
+          top = (!SPILL || i < STACK) ? stk[i * BLOCK] : spill[(size_t)(i - STACK) * spill_lanes];
+        }
         const bool popn = can && top >= 0;
         const bool popl = can && top < 0 && ts.pend == 0;
         ts.node = popn ? top : ts.node;
@@ -335,6 +342,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         for (int k = 0; k < 4; ++k) {
           if ((push >> k) & 1u) {
             if (sp < STACK) stk[sp * BLOCK] = CW[k];
+            else if (SPILL) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // within Flat::stack_need
             ++sp;
           }
         }
@@ -527,10 +535,11 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   return true;
 }
 
-template <bool COUNT, int STACK, int OCC, uint32_t FEAT>
+template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT>
 __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   __shared__ int32_t stk_all[STACK * BLOCK];
   int32_t* stk = stk_all + threadIdx.x;
+  int32_t* spill = a.spill + (size_t)blockIdx.x * BLOCK + threadIdx.x;  // unused unless spill_depth > 0
   const uint32_t lane = threadIdx.x & 63u;
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
@@ -590,7 +599,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     }
     {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
-      trace_run<COUNT, STACK, FEAT>(S, st.ray, ts, stk, cnt, quota);
+      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota);
     }
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
     ts.on = false;
@@ -755,6 +764,7 @@ void release(Scene& s) {
     if (c.block) hipFree(c.block);
     if (c.counters) hipFree(c.counters);
     if (c.sbuf) hipFree(c.sbuf);
+    if (c.spill) hipFree(c.spill);
   }
   s.dev.clear();
 }
@@ -767,29 +777,36 @@ static DeviceCopy* find_copy(Scene& s, int device) {
 
 constexpr uint64_t MAX_PASS_PATHS = 1ull << 30;  // 12.9 GB of ordered samples per pass
 
-// Variants of the path kernel: feature set x LDS stack depth (by the scene's BVH depth) x the waves
-// per SIMD the register allocator must allow.  Sphere-only scenes (jumpy-balls) get the
-// specialised kernel; everything else the generic one.  RTW_OCC=4|6|8 overrides the occupancy
-// target of the specialised kernel (tuning knob).
+// Variants of the path kernel: feature set x the waves per SIMD the register allocator must allow.
+// Sphere-only scenes (jumpy-balls) get the specialised kernel; everything else the generic one.
+// Trees whose push bound exceeds the LDS stack get the SPILL variant.  RTW_OCC=6 selects a
+// 6-waves/SIMD build of the specialised kernel (tuning knob; it spills registers);
+// RTW_STACK_LDS=4 selects a generic kernel with a 4-entry LDS stack, so that the HBM spill path
+// runs on every scene (tests/test_gpu_parity.py).
 typedef void (*path_fn)(RenderArgs);
 static int env_int(const char* k, int dflt) {
   const char* e = getenv(k);
   return e ? atoi(e) : dflt;
 }
 template <bool C>
-static path_fn pick_kernel(uint32_t feat, bool shallow) {
-  if ((feat & ~F_SPHERES) == 0 && shallow) {
-    switch (env_int("RTW_OCC", 4)) {
-      case 4: return dev::path_kernel<C, dev::STACK_SHALLOW, 4, F_SPHERES>;
-      case 8: return dev::path_kernel<C, dev::STACK_SHALLOW, 8, F_SPHERES>;
-      default: return dev::path_kernel<C, dev::STACK_SHALLOW, 6, F_SPHERES>;
-    }
+static path_fn pick_kernel(uint32_t feat, uint32_t need) {
+  using namespace dev;
+  if (env_int("RTW_STACK_LDS", 0) == 4) return path_kernel<C, 4, true, 4, F_ALL>;  // spill-path test
+  const bool spill = need > (uint32_t)STACK_LDS;
+  if ((feat & ~F_SPHERES) == 0) {
+    if (spill) return path_kernel<C, STACK_LDS, true, 4, F_SPHERES>;
+    if (env_int("RTW_OCC", 4) == 6 && need <= (uint32_t)STACK_LDS6) return path_kernel<C, STACK_LDS6, false, 6, F_SPHERES>;
+    return path_kernel<C, STACK_LDS, false, 4, F_SPHERES>;
   }
-  if ((feat & ~F_SPHERES) == 0) return dev::path_kernel<C, dev::STACK_DEEP, 4, F_SPHERES>;
-  return shallow ? dev::path_kernel<C, dev::STACK_SHALLOW, 4, F_ALL> : dev::path_kernel<C, dev::STACK_DEEP, 4, F_ALL>;
+  return spill ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>;
 }
-static path_fn path_kernel_ptr(bool count, uint32_t feat, bool shallow) {
-  return count ? pick_kernel<true>(feat, shallow) : pick_kernel<false>(feat, shallow);
+static uint32_t stack_lds(uint32_t feat, uint32_t need) {
+  if (env_int("RTW_STACK_LDS", 0) == 4) return 4;
+  const bool occ6 = (feat & ~F_SPHERES) == 0 && env_int("RTW_OCC", 4) == 6 && need <= (uint32_t)dev::STACK_LDS6;
+  return occ6 ? dev::STACK_LDS6 : dev::STACK_LDS;
+}
+static path_fn path_kernel_ptr(bool count, uint32_t feat, uint32_t need) {
+  return count ? pick_kernel<true>(feat, need) : pick_kernel<false>(feat, need);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, bool count) {
@@ -854,9 +871,20 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const bool shallow = sc.flat.stack_need <= (uint32_t)dev::STACK_SHALLOW;
-    const path_fn fn = path_kernel_ptr(count, sc.flat.features, shallow);
+    const path_fn fn = path_kernel_ptr(count, sc.flat.features, sc.flat.stack_need);
     const int grid = resident_grid(c, fn, count);
+    const uint32_t lds = stack_lds(sc.flat.features, sc.flat.stack_need);
+    a.spill_depth = sc.flat.stack_need > lds ? sc.flat.stack_need - lds : 0;
+    a.spill_lanes = (uint32_t)grid * dev::BLOCK;
+    const size_t spill_bytes = (size_t)a.spill_depth * a.spill_lanes * sizeof(int32_t);
+    if (spill_bytes > c.spill_bytes) {  // first render of a deep tree only
+      if (c.spill) HIPCHK(hipFree(c.spill), "hipFree(stack spill)");
+      c.spill = nullptr;
+      c.spill_bytes = 0;
+      HIPCHK(hipMalloc((void**)&c.spill, spill_bytes), "hipMalloc(stack spill)");
+      c.spill_bytes = spill_bytes;
+    }
+    a.spill = c.spill;
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;

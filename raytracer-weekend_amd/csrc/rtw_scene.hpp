@@ -74,8 +74,10 @@ struct DeviceCopy {
   unsigned long long* counters = nullptr;  // 16 x u64: [0..8] stats, [15] path queue
   float* sbuf = nullptr;                   // ordered per-sample radiance (3 planes)
   uint64_t sbuf_paths = 0;
+  int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)
+  size_t spill_bytes = 0;
   int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting); the
-                                           // variant is fixed per scene (features, depth)
+                                           // variant is fixed per scene (features)
 };
 
 struct Scene {

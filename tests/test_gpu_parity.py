@@ -93,3 +93,13 @@ def test_error_paths(gpu):
         rtw.Raytracer(s, cam, (0, 0, 0), 1, 1, 1).render()  # lib.rs:84-85 divides by w-1
     with pytest.raises(rtw.RtwError):
         s.sphere((0, 0, 0), 1, m)  # scene immutable after commit
+
+
+@pytest.mark.parametrize("name,aspect,w,h,spp", [SCENES[0], SCENES[2], SCENES[3]])
+def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
+    """A 4-entry LDS stack pushes every deeper entry through the HBM spill area
+    (RenderArgs::spill); the image must not change."""
+    monkeypatch.setenv("RTW_STACK_LDS", "4")
+    g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
+    assert st["rays"] == rays
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
