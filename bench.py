@@ -282,7 +282,8 @@ def main() -> int:
                          "alg_bytes_per_ray": round(alg_bytes_frame / max(1, frame_rays), 2),
                          "node_fetches_per_ray": round(nodes_r / max(1, rays_r), 3),
                          "prim_tests_per_ray": round(float(counts[2:8].sum()) / max(1, rays_r), 3),
-                         "simd_util_rank0": {k: (round(v, 3) if v else v) for k, v in st["simd_util"].items()}},
+                         "simd_util_rank0": {k: (round(v, 3) if v else v) for k, v in st["simd_util"].items()},
+                         "phase_share_rank0": {k: (round(v, 3) if v else v) for k, v in st["phase_share"].items()}},
             "paths_per_sec": round(w * h * spp * args.steps / dt, 1),
         }
         if world == 1 and not args.no_cpu_baseline:

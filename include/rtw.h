@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 enum {
   RTW_OK = 0,
@@ -62,6 +62,9 @@ typedef struct {
   /* RTW_FLAG_COUNT_TRAVERSAL: SIMD utilisation, pairs of (wave executions, active lanes) for
    * the BVH node loop, primitive tests and path segments */
   uint64_t simd[6];
+  /* RTW_FLAG_COUNT_TRAVERSAL: wave-cycles (s_memtime) spent in path regeneration, closest-hit
+   * traversal and shading, and in the whole path kernel, summed over waves */
+  uint64_t phase_cycles[4];
 } rtw_stats;
 
 enum { RTW_FLAG_COUNT_TRAVERSAL = 1 };

@@ -51,7 +51,8 @@ class rtw_camera(C.Structure):  # include/rtw.h, camera.rs:9-20
 class rtw_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("kernel_ms", C.c_double),
                 ("total_ms", C.c_double), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
-                ("prim_tests_by_type", C.c_uint64 * 6), ("simd", C.c_uint64 * 6)]
+                ("prim_tests_by_type", C.c_uint64 * 6), ("simd", C.c_uint64 * 6),
+                ("phase_cycles", C.c_uint64 * 4)]
 
     def as_dict(self) -> dict:
         return {"rays": int(self.rays), "paths": int(self.paths), "kernel_ms": float(self.kernel_ms),
@@ -59,7 +60,9 @@ class rtw_stats(C.Structure):
                 "prim_tests": int(self.prim_tests),
                 "prim_tests_by_type": [int(x) for x in self.prim_tests_by_type],
                 "simd_util": {k: (self.simd[2 * q + 1] / (64.0 * self.simd[2 * q]) if self.simd[2 * q] else None)
-                              for q, k in enumerate(("node_loop", "prim_tests", "segments"))}}
+                              for q, k in enumerate(("node_loop", "prim_tests", "segments"))},
+                "phase_share": {k: (self.phase_cycles[q] / self.phase_cycles[3] if self.phase_cycles[3] else None)
+                                for q, k in enumerate(("regen", "trace", "shade"))}}
 
 
 _F = C.POINTER(C.c_float)

@@ -503,6 +503,7 @@ int flatten(Scene& s) {
     Collapse col{f.nodes, f.nodes4};
     uint32_t bound = 0;
     col.build(0, &bound);
+    if (f.nodes4.size() >= (1u << 25)) return fail(RTW_EINVAL, "BVH4 too large for 32-bit node offsets");
     f.stack_need = bound;  // entries beyond the kernel's LDS stack spill to a per-lane HBM area
     if (f.stack_need > 4096) return fail(RTW_EINVAL, "BVH4 stack bound %u is unreasonable", f.stack_need);
     // self-check: every node4 reached once, every BVH prim covered once

@@ -91,19 +91,26 @@ __device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi) {  /
     sc = __uint_as_float(__float_as_uint(sc) - 1u);
   }
 }
+// gen_range(s, -1, 1) without the retry loop: v01 = m * 2^-23 (m < 2^23), so v01 * 2 - 1 =
+// (m - 2^22) * 2^-22 is exact and at most 1 - 2^-22 < 1; the retry never fires (checked for
+// every m in tests/test_oracle_kat.py::test_pm1_never_retries).
+__device__ __forceinline__ float gen_pm1(uint64_t& s) {
+  const float v01 = __uint_as_float((pcg_next(s) >> 9) | 0x3F800000u) - 1.0f;
+  return v01 * 2.0f + -1.0f;
+}
 __device__ __forceinline__ V3 rand_in_unit_sphere(uint64_t& s) {  // vec3.rs:101-108
   for (;;) {
-    float x = gen_range(s, -1.0f, 1.0f);
-    float y = gen_range(s, -1.0f, 1.0f);
-    float z = gen_range(s, -1.0f, 1.0f);
+    float x = gen_pm1(s);
+    float y = gen_pm1(s);
+    float z = gen_pm1(s);
     V3 p = mk(x, y, z);
     if (len2(p) < 1.0f) return p;
   }
 }
 __device__ __forceinline__ V3 rand_in_unit_disk(uint64_t& s) {  // vec3.rs:124-131
   for (;;) {
-    float x = gen_range(s, -1.0f, 1.0f);
-    float y = gen_range(s, -1.0f, 1.0f);
+    float x = gen_pm1(s);
+    float y = gen_pm1(s);
     V3 p = mk(x, y, 0.0f);
     if (len2(p) < 1.0f) return p;
   }
@@ -274,9 +281,11 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   };
   const V3 inv = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
-  // near / far plane float offsets inside DevNode4 by the ray's direction signs
-  const int nx = inv.x < 0.f ? 4 : 0, ny = (inv.y < 0.f ? 4 : 0) + 8, nz = (inv.z < 0.f ? 4 : 0) + 16;
-  const int fx = nx ^ 4, fy = ny ^ 4, fz = nz ^ 4;
+  // near / far plane byte offsets inside DevNode4 by the ray's direction signs (32-bit offsets
+  // from the uniform table base: the loads take the SGPR-base + VGPR-offset form)
+  const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
+  const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
+  const char* const NB = reinterpret_cast<const char*>(S.nodes);
   // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
   for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
     for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
@@ -295,11 +304,14 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       }
       if (!__any(ts.node >= 0 && ts.pend == 0)) break;
       if (ts.node >= 0) {
-        const float* N = reinterpret_cast<const float*>(S.nodes + ts.node);
-        const float4 qnx = *reinterpret_cast<const float4*>(N + nx), qfx = *reinterpret_cast<const float4*>(N + fx);
-        const float4 qny = *reinterpret_cast<const float4*>(N + ny), qfy = *reinterpret_cast<const float4*>(N + fy);
-        const float4 qnz = *reinterpret_cast<const float4*>(N + nz), qfz = *reinterpret_cast<const float4*>(N + fz);
-        const int4 cw = *reinterpret_cast<const int4*>(N + 24);
+        const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
+        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
+        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
+        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
+        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
+        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
+        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
+        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + 96u));
         if (COUNT) { cnt[0]++; simd_tick(cnt, 8, 9); }
         const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
         float tn[4];
@@ -340,11 +352,18 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         int32_t sp = ts.sp;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if ((push >> k) & 1u) {
-            if (sp < STACK) stk[sp * BLOCK] = CW[k];
-            else if (SPILL) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // within Flat::stack_need
-            ++sp;
+          const bool pk = (push >> k) & 1u;
+          if (SPILL) {
+            if (pk) {
+              if (sp < STACK) stk[sp * BLOCK] = CW[k];
+              else spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // sp < Flat::stack_need
+            }
+          } else {
+            // branch-free: a child that is not pushed is written where the next push (or nothing)
+            // lands, i.e. at or above the final top, never below it; rows 0..STACK exist
+            stk[sp * BLOCK] = CW[k];
           }
+          sp += pk ? 1 : 0;
         }
         ts.sp = sp;
         ts.node = next;
@@ -537,7 +556,7 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
 
 template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT>
 __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
-  __shared__ int32_t stk_all[STACK * BLOCK];
+  __shared__ int32_t stk_all[(STACK + 1) * BLOCK];  // + 1: trace_run's branch-free push
   int32_t* stk = stk_all + threadIdx.x;
   int32_t* spill = a.spill + (size_t)blockIdx.x * BLOCK + threadIdx.x;  // unused unless spill_depth > 0
   const uint32_t lane = threadIdx.x & 63u;
@@ -555,7 +574,18 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   st.pid = 0;
   st.rng = 0;
   st.depth = 0;
+  uint64_t ph[3] = {0, 0, 0};  // COUNT: wave-cycles in regeneration / traversal / shading
+  const uint64_t t_start = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t t_mark = t_start;
+  auto phase = [&](int k) {
+    if (COUNT) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph[k] += t - t_mark;
+      t_mark = t;
+    }
+  };
   for (;;) {
+    phase(2);
     // ---- regeneration: compact new path ids into the idle lanes
     const uint64_t need = __ballot(!has);
     if (need != 0 && !exhausted) {
@@ -591,6 +621,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       if (exhausted) break;
       continue;  // every id handed out this round was an off-image pixel: draw again
     }
+    phase(0);
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
     if (!ts.on) {
@@ -601,6 +632,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota);
     }
+    phase(1);
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
     ts.on = false;
     if (COUNT) simd_tick(cnt, 12, 13);
@@ -657,6 +689,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
   if (lane == 0 && tot) atomicAdd(a.counters, tot);
   if (COUNT) {
+    phase(2);
+    if (lane == 0) {
+      for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
+      atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
+    }
     for (int q = 0; q < 14; ++q) {
       unsigned long long c = cnt[q];
       for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -738,7 +775,7 @@ int upload(Scene& s, int device) {
     c.bytes = blob.size();
     HIPCHK(hipMalloc(&c.block, c.bytes), "hipMalloc(scene)");
     HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
-    HIPCHK(hipMalloc((void**)&c.counters, 16 * sizeof(unsigned long long)), "hipMalloc(counters)");
+    HIPCHK(hipMalloc((void**)&c.counters, 32 * sizeof(unsigned long long)), "hipMalloc(counters)");
     uint8_t* base = (uint8_t*)c.block;
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
@@ -852,8 +889,8 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   a.seed_hash = z ^ (z >> 31);
   a.out = d_out;
   a.counters = c.counters;
-  a.queue = c.counters + 15;
-  HIPCHK(hipMemsetAsync(c.counters, 0, 16 * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  a.queue = c.counters + 31;
+  HIPCHK(hipMemsetAsync(c.counters, 0, 32 * sizeof(unsigned long long), stream), "hipMemsetAsync");
   if (ev0) HIPCHK(hipEventRecord(ev0, stream), "hipEventRecord");
   if (n_slots && (spp == 0 || max_depth == 0)) {  // lib.rs:83 loops 0 times / :98 returns black
     size_t n = d_tiles ? (size_t)n_slots * 64 * 3 : (size_t)w * h * 3;
@@ -903,7 +940,7 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
 static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1, uint64_t paths,
                       rtw_stats* st) {
   HIPCHK(hipStreamSynchronize(stream), "render_kernel");
-  unsigned long long cnt[16];
+  unsigned long long cnt[32];
   HIPCHK(hipMemcpy(cnt, c.counters, sizeof cnt, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
   float ms = 0.f;
   if (ev0 && ev1) HIPCHK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
@@ -914,6 +951,7 @@ static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEven
   st->prim_tests = cnt[2];
   for (int k = 0; k < 6; ++k) st->prim_tests_by_type[k] = cnt[3 + k];
   for (int k = 0; k < 6; ++k) st->simd[k] = cnt[9 + k];
+  for (int k = 0; k < 4; ++k) st->phase_cycles[k] = cnt[16 + k];
   return RTW_OK;
 }
 

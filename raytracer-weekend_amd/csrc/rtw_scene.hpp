@@ -71,7 +71,7 @@ struct DeviceCopy {
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
-  unsigned long long* counters = nullptr;  // 16 x u64: [0..8] stats, [15] path queue
+  unsigned long long* counters = nullptr;  // 32 x u64: [0..19] stats, [31] path queue
   float* sbuf = nullptr;                   // ordered per-sample radiance (3 planes)
   uint64_t sbuf_paths = 0;
   int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)

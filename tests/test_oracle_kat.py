@@ -148,3 +148,13 @@ def test_checker_sign_fast_path_sample():
         par = np.floor(arr.astype(np.float64) * 0.31830988618379067154).astype(np.int64) & 1
         sgn = np.array([libm.sinf(float(x)) < 0 for x in arr])
         assert np.array_equal(par.astype(bool), sgn)
+
+
+def test_pm1_never_retries():
+    """gen_range(-1, 1) (UniformFloat::sample_single) never takes its retry branch: the kernel's
+    gen_pm1 relies on it.  Every 23-bit mantissa draw, evaluated in f32 as mul-then-add."""
+    m = np.arange(1 << 23, dtype=np.uint32)
+    v01 = ((m | np.uint32(0x3F800000)).view(np.float32) - np.float32(1.0)).astype(np.float32)
+    r = (v01 * np.float32(2.0)).astype(np.float32) + np.float32(-1.0)
+    assert r.dtype == np.float32
+    assert float(r.max()) < 1.0 and float(r.min()) == -1.0
