@@ -115,6 +115,9 @@ EXPORTED_SYMBOLS = tuple(_SIGS)
 _lib = None
 
 
+ABI_VERSION = 2  # include/rtw.h RTW_ABI_VERSION
+
+
 def lib() -> C.CDLL:
     """Load librtw_amd.so (fails loudly: there is no fallback path)."""
     global _lib
@@ -134,6 +137,8 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.rtw_abi_version() != ABI_VERSION:  # rtw_stats layout etc. must match this mirror
+            raise RtwError(RTW_ESTATE, f"{LIB_PATH} has ABI {L.rtw_abi_version()}, this mirror {ABI_VERSION}")
         _lib = L
     return _lib
 

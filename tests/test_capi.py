@@ -23,7 +23,7 @@ def test_every_declared_symbol_is_exported(rtw):
     missing = [f for f in declared if not hasattr(lib, f)]
     assert not missing, missing
     assert set(declared) == set(rtw.EXPORTED_SYMBOLS), set(declared) ^ set(rtw.EXPORTED_SYMBOLS)
-    assert lib.rtw_abi_version() == 1
+    assert lib.rtw_abi_version() == rtw.ABI_VERSION
 
 
 def test_camera_matches_oracle(rtw, orc):
@@ -118,3 +118,9 @@ def test_image_height_rule(rtw):
     assert rtw.image_height(1920) == 1080
     assert rtw.image_height(3840) == 2160
     assert rtw.camera_aspect(1920, 1080) == np.float32(1920) / np.float32(1080)
+
+
+def test_abi_version_matches_header(rtw):
+    import pathlib
+    text = (pathlib.Path(__file__).resolve().parents[1] / "include" / "rtw.h").read_text()
+    assert int(re.search(r"#define RTW_ABI_VERSION (\d+)", text).group(1)) == rtw.ABI_VERSION
