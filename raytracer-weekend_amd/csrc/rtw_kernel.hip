@@ -33,11 +33,12 @@ namespace dev {
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
-// LDS traversal-stack entries per lane.  160 KB of LDS per CU holds 5 blocks of 256 lanes x 32
-// entries, so the stack never limits occupancy below the 4-5 waves/SIMD the registers allow; a tree
-// whose worst-case push bound (Flat::stack_need) is deeper spills the excess to HBM (RenderArgs::spill).
+// LDS traversal-stack entries per lane (+ 1 scratch row).  At the 5 waves/SIMD the default
+// variants are register-allocated for, 160 KB of LDS per CU holds 5 blocks of 256 lanes x 25 rows;
+// a tree whose worst-case push bound (Flat::stack_need) is deeper keeps the excess in HBM
+// (RenderArgs::spill).  STACK_LDS (33 rows) is for the 4-waves/SIMD tuning variants.
 constexpr int STACK_LDS = 32;
-constexpr int STACK_LDS6 = 24;  // 6 waves/SIMD variant
+constexpr int STACK_LDS5 = 24;
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -294,7 +295,8 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         int32_t top = 0;
         if (can) {
           const int32_t i = ts.sp - 1;
-          top = (!SPILL || i < STACK) ? stk[i * BLOCK] : spill[(size_t)(i - STACK) * spill_lanes];
+          top = stk[(SPILL ? min(i, STACK) : i) * BLOCK];
+          if (SPILL && i >= STACK) top = spill[(size_t)(i - STACK) * spill_lanes];  // rare
         }
         const bool popn = can && top >= 0;
         const bool popl = can && top < 0 && ts.pend == 0;
@@ -353,16 +355,11 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const bool pk = (push >> k) & 1u;
-          if (SPILL) {
-            if (pk) {
-              if (sp < STACK) stk[sp * BLOCK] = CW[k];
-              else spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // sp < Flat::stack_need
-            }
-          } else {
-            // branch-free: a child that is not pushed is written where the next push (or nothing)
-            // lands, i.e. at or above the final top, never below it; rows 0..STACK exist
-            stk[sp * BLOCK] = CW[k];
-          }
+          // branch-free: a child that is not pushed is written where the next push (or nothing)
+          // lands, i.e. at or above the final top, never below it.  Rows 0..STACK exist; with
+          // SPILL, row STACK is scratch and entries from STACK up live in HBM (sp < stack_need).
+          stk[(SPILL ? min(sp, STACK) : sp) * BLOCK] = CW[k];
+          if (SPILL && pk && sp >= STACK) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // rare
           sp += pk ? 1 : 0;
         }
         ts.sp = sp;
@@ -816,8 +813,8 @@ constexpr uint64_t MAX_PASS_PATHS = 1ull << 30;  // 12.9 GB of ordered samples p
 
 // Variants of the path kernel: feature set x the waves per SIMD the register allocator must allow.
 // Sphere-only scenes (jumpy-balls) get the specialised kernel; everything else the generic one.
-// Trees whose push bound exceeds the LDS stack get the SPILL variant.  RTW_OCC=6 selects a
-// 6-waves/SIMD build of the specialised kernel (tuning knob; it spills registers);
+// Trees whose push bound exceeds the LDS stack get the SPILL variant.  Default: 5 waves/SIMD.
+// Tuning knobs: RTW_OCC=4 (33-row stack) or RTW_OCC=6 (specialised kernel; spills registers);
 // RTW_STACK_LDS=4 selects a generic kernel with a 4-entry LDS stack, so that the HBM spill path
 // runs on every scene (tests/test_gpu_parity.py).
 typedef void (*path_fn)(RenderArgs);
@@ -829,18 +826,27 @@ template <bool C>
 static path_fn pick_kernel(uint32_t feat, uint32_t need) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return path_kernel<C, 4, true, 4, F_ALL>;  // spill-path test
-  const bool spill = need > (uint32_t)STACK_LDS;
-  if ((feat & ~F_SPHERES) == 0) {
-    if (spill) return path_kernel<C, STACK_LDS, true, 4, F_SPHERES>;
-    if (env_int("RTW_OCC", 4) == 6 && need <= (uint32_t)STACK_LDS6) return path_kernel<C, STACK_LDS6, false, 6, F_SPHERES>;
-    return path_kernel<C, STACK_LDS, false, 4, F_SPHERES>;
+  const bool sph = (feat & ~F_SPHERES) == 0;
+  switch (env_int("RTW_OCC", 5)) {
+    case 4: {
+      const bool sp = need > (uint32_t)STACK_LDS;
+      if (sph) return sp ? path_kernel<C, STACK_LDS, true, 4, F_SPHERES> : path_kernel<C, STACK_LDS, false, 4, F_SPHERES>;
+      return sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>;
+    }
+    case 6:
+      if (sph && need <= (uint32_t)STACK_LDS5) return path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>;
+      [[fallthrough]];
+    default: {
+      const bool sp = need > (uint32_t)STACK_LDS5;
+      if (sph) return sp ? path_kernel<C, STACK_LDS5, true, 5, F_SPHERES> : path_kernel<C, STACK_LDS5, false, 5, F_SPHERES>;
+      return sp ? path_kernel<C, STACK_LDS5, true, 5, F_ALL> : path_kernel<C, STACK_LDS5, false, 5, F_ALL>;
+    }
   }
-  return spill ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>;
 }
 static uint32_t stack_lds(uint32_t feat, uint32_t need) {
+  (void)feat; (void)need;
   if (env_int("RTW_STACK_LDS", 0) == 4) return 4;
-  const bool occ6 = (feat & ~F_SPHERES) == 0 && env_int("RTW_OCC", 4) == 6 && need <= (uint32_t)dev::STACK_LDS6;
-  return occ6 ? dev::STACK_LDS6 : dev::STACK_LDS;
+  return env_int("RTW_OCC", 5) == 4 ? dev::STACK_LDS : dev::STACK_LDS5;
 }
 static path_fn path_kernel_ptr(bool count, uint32_t feat, uint32_t need) {
   return count ? pick_kernel<true>(feat, need) : pick_kernel<false>(feat, need);
