@@ -220,11 +220,11 @@ def main() -> int:
             if not same:
                 raise SystemExit("gathered frame differs from the single-device render")
     torch.cuda.synchronize()
+    scene.path_kernel_times(dev)  # forget the untimed launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms = []
     for _ in range(args.steps):
         render_frame(True)
         frame_end()
@@ -237,8 +237,12 @@ def main() -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    kernel_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(launches)]  # last step's launches
-    frame_kernel_ms = float(sum(kernel_ms))
+    call_ms = float(sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(launches)))  # last step: path + reduce
+    # path_kernel alone: the library's HIP events around each launch on this stream, all K steps
+    pk = scene.path_kernel_times(dev)  # the last min(64, K * launches) launches
+    if len(pk) != min(64, args.steps * launches) or len(pk) % launches:
+        raise SystemExit(f"expected {args.steps * launches} path-kernel timings, got {len(pk)}")
+    frame_kernel_ms = float(sum(pk)) / (len(pk) // launches)
 
     value = frame_rays * args.steps / dt / 1e6
     # roofline of the render kernel (this rank): algorithmic bytes per launch / avg launch time
@@ -279,6 +283,7 @@ def main() -> int:
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": "path_kernel",
                          "kernel_ms_per_frame": round(frame_kernel_ms, 3),
+                         "render_call_ms_last_frame": round(call_ms, 3),
                          "alg_bytes_per_ray": round(alg_bytes_frame / max(1, frame_rays), 2),
                          "node_fetches_per_ray": round(nodes_r / max(1, rays_r), 3),
                          "prim_tests_per_ray": round(float(counts[2:8].sum()) / max(1, rays_r), 3),

@@ -174,6 +174,12 @@ int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const flo
 int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* d_tile_ids,
                             uint32_t n_tiles, const float* d_packed, float* d_image, void* stream);
 
+/* Device time (ms, HIP events on the render stream) of the most recent path-kernel launches of
+ * rtw_render / rtw_render_device on `device`, oldest first: at most max_n of the last 64, written
+ * to ms[]; returns how many (>= 0) or an error, and forgets them.  Waits for those launches.
+ * (Benchmark hook: the render call itself also enqueues the in-order sample reduction.) */
+int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
+
 /* console_app/src/main.rs:68-90 tonemap: sqrt(sum/spp), clamp [0, 0.999], u8(255.999*c). */
 int rtw_tonemap(const float* rgb_sum, uint32_t n_pixels, uint32_t spp, uint8_t* rgb8);
 

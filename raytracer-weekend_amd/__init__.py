@@ -101,6 +101,7 @@ _SIGS = {
     "rtw_render_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_uint32, C.c_uint64, _U32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
+    "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
     "rtw_unpack_tiles_device": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
@@ -340,6 +341,14 @@ class Scene:
                 return out
             out.append(np.ctypeslib.as_array(px, shape=(h.value * w.value * 3,)).copy())
             k += 1
+
+    def path_kernel_times(self, device: int = -1, max_n: int = 64) -> list:
+        """Device ms of the recent path-kernel launches on `device` (oldest first; waits for them)."""
+        buf = (C.c_float * max_n)()
+        n = lib().rtw_path_kernel_times(self._p, device, buf, max_n)
+        if n < 0:
+            _check(n)
+        return [float(buf[q]) for q in range(n)]
 
     def info(self, what: int) -> int:
         return int(lib().rtw_scene_info(self._p, what))

@@ -799,6 +799,9 @@ void release(Scene& s) {
     if (c.counters) hipFree(c.counters);
     if (c.sbuf) hipFree(c.sbuf);
     if (c.spill) hipFree(c.spill);
+    for (auto& e : c.kev)
+      for (void* x : e)
+        if (x) hipEventDestroy(static_cast<hipEvent_t>(x));
   }
   s.dev.clear();
 }
@@ -933,8 +936,15 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
       a.slot_base = base;
       a.n_paths = (uint64_t)ns * per_slot;
       if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
+      hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
+      if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
+      if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
+      HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
       hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
       HIPCHK(hipGetLastError(), "path_kernel launch");
+      HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
+      c.kev_head = (c.kev_head + 1) % 64u;
+      c.kev_count = std::min(c.kev_count + 1u, 64u);
       hipLaunchKernelGGL(dev::reduce_kernel, dim3((ns * 64u + 255u) / 256u), dim3(256), 0, stream, a, ns);
       HIPCHK(hipGetLastError(), "reduce_kernel launch");
     }
@@ -1033,6 +1043,29 @@ int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const flo
   }
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
+  hipSetDevice(prev);
+  return rc;
+}
+
+int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
+  if (!s || (!ms && max_n)) return fail(RTW_EINVAL, "NULL argument");
+  DeviceCopy* c = find_copy(s->s, device);
+  if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
+  int prev = 0;
+  hipGetDevice(&prev);
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  const uint32_t n = std::min(c->kev_count, max_n);
+  int rc = (int)n;
+  for (uint32_t q = 0; q < n; ++q) {  // the n most recent, oldest first
+    hipEvent_t* e = reinterpret_cast<hipEvent_t*>(c->kev[(c->kev_head + 64u - n + q) % 64u]);
+    hipError_t err = hipEventSynchronize(e[1]);
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms[q], e[0], e[1]);
+    if (err != hipSuccess) {
+      rc = hip_fail(err, "path-kernel events");
+      break;
+    }
+  }
+  c->kev_count = 0;
   hipSetDevice(prev);
   return rc;
 }

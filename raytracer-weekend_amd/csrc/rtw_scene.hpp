@@ -76,6 +76,9 @@ struct DeviceCopy {
   uint64_t sbuf_paths = 0;
   int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)
   size_t spill_bytes = 0;
+  void* kev[64][2] = {};                   // hipEvent_t pairs around path-kernel launches (ring,
+                                           // rtw_path_kernel_times)
+  uint32_t kev_head = 0, kev_count = 0;
   int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting); the
                                            // variant is fixed per scene (features)
 };

@@ -10,7 +10,7 @@ mkdir -p $R/gpurun_out
   python3 $R/bench.py $ARGS > $R/gpurun_out/${TAG}kt.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv --kernel-include-regex "path_kernel|reduce_kernel" \
-    -d $R/gpurun_out/${TAG}pmc_$c -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+    -d $R/gpurun_out/${TAG}pmc_$c -o pmc -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline $PMC_ARGS \
     > $R/gpurun_out/${TAG}pmc_$c.log 2>&1 || exit $?
 done
 find $R/gpurun_out -name "*.csv" | head -20

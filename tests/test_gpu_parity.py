@@ -103,3 +103,16 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
     g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
     assert st["rays"] == rays
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def test_path_kernel_times(gpu):
+    rtw = gpu
+    s = rtw.Scene()
+    cam, bg = s.preset("cornell-box", 1.0, seed=3)
+    s.commit(device=0)
+    rt = rtw.Raytracer(s, cam, bg, 16, 16, 2, seed=1)
+    rt.render()
+    rt.render()
+    t = s.path_kernel_times(0)
+    assert len(t) == 2 and all(x > 0 for x in t)
+    assert s.path_kernel_times(0) == []  # consumed
