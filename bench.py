@@ -239,10 +239,13 @@ def main() -> int:
         dt = float(t.item())
     call_ms = float(sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(launches)))  # last step: path + reduce
     # path_kernel alone: the library's HIP events around each launch on this stream, all K steps
-    pk = scene.path_kernel_times(dev)  # the last min(64, K * launches) launches
-    if len(pk) != min(64, args.steps * launches) or len(pk) % launches:
-        raise SystemExit(f"expected {args.steps * launches} path-kernel timings, got {len(pk)}")
-    frame_kernel_ms = float(sum(pk)) / (len(pk) // launches)
+    # (a render call splits a frame larger than MAX_PASS_PATHS into several passes, one launch each)
+    pk = scene.path_kernel_times(dev)  # the last min(64, K * launches * passes) launches
+    if not pk or len(pk) >= 64 or len(pk) % (args.steps * launches):
+        raise SystemExit(f"path-kernel timings: got {len(pk)} for {args.steps} steps x {launches} calls "
+                         "(ring of 64 overflowed or launches missing; lower --steps)")
+    passes = len(pk) // (args.steps * launches)
+    frame_kernel_ms = float(sum(pk)) / args.steps
 
     value = frame_rays * args.steps / dt / 1e6
     # roofline of the render kernel (this rank): algorithmic bytes per launch / avg launch time
@@ -283,6 +286,8 @@ def main() -> int:
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": "path_kernel",
                          "kernel_ms_per_frame": round(frame_kernel_ms, 3),
+                         "kernel_launches_per_frame": launches * passes,
+                         "alg_bytes_per_launch": round(alg_bytes_rank / (launches * passes)),
                          "render_call_ms_last_frame": round(call_ms, 3),
                          "alg_bytes_per_ray": round(alg_bytes_frame / max(1, frame_rays), 2),
                          "node_fetches_per_ray": round(nodes_r / max(1, rays_r), 3),

@@ -421,6 +421,7 @@ int64_t rtw_scene_info(const rtw_scene* s, int what) {
     case 3: return (int64_t)sc.flat.nodes4.size();
     case 7: return (int64_t)sc.flat.nodes.size();
     case 8: return (int64_t)sc.flat.stack_need;
+    case 9: return (int64_t)sc.flat.features;
     case 4: return (int64_t)sc.flat.depth;
     case 5: return (int64_t)sc.flat.always.size();
     case 6: return (int64_t)sc.flat.insts.size();

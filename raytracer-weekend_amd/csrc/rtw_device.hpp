@@ -104,7 +104,12 @@ enum Feature : uint32_t {
   F_LIGHT = 1u << 12,
 };
 constexpr uint32_t F_ALL = (1u << 13) - 1;
+// Kernel variants (the smallest superset of a scene's features is launched): sphere worlds
+// (jumpy-balls), rect/instance worlds with solid colours (cornell-box), diffuse meshes (cow,
+// monument), and everything.
 constexpr uint32_t F_SPHERES = F_SPHERE | F_MSPHERE | F_CHECKER | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
+constexpr uint32_t F_BOXES = F_RECT | F_INST | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
+constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F_IMAGE | F_LAMBERT | F_LIGHT;
 
 struct DevScene {
   const DevNode4* nodes;

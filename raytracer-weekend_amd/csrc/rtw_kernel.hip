@@ -825,6 +825,11 @@ static int env_int(const char* k, int dflt) {
   const char* e = getenv(k);
   return e ? atoi(e) : dflt;
 }
+template <bool C, uint32_t F>
+static path_fn pick5(uint32_t need) {
+  using namespace dev;
+  return need > (uint32_t)STACK_LDS5 ? path_kernel<C, STACK_LDS5, true, 5, F> : path_kernel<C, STACK_LDS5, false, 5, F>;
+}
 template <bool C>
 static path_fn pick_kernel(uint32_t feat, uint32_t need) {
   using namespace dev;
@@ -839,11 +844,12 @@ static path_fn pick_kernel(uint32_t feat, uint32_t need) {
     case 6:
       if (sph && need <= (uint32_t)STACK_LDS5) return path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>;
       [[fallthrough]];
-    default: {
-      const bool sp = need > (uint32_t)STACK_LDS5;
-      if (sph) return sp ? path_kernel<C, STACK_LDS5, true, 5, F_SPHERES> : path_kernel<C, STACK_LDS5, false, 5, F_SPHERES>;
-      return sp ? path_kernel<C, STACK_LDS5, true, 5, F_ALL> : path_kernel<C, STACK_LDS5, false, 5, F_ALL>;
-    }
+    default:
+      if (env_int("RTW_GENERIC", 0)) return pick5<C, F_ALL>(need);  // parity of the generic kernel
+      if (sph) return pick5<C, F_SPHERES>(need);
+      if ((feat & ~F_BOXES) == 0) return pick5<C, F_BOXES>(need);
+      if ((feat & ~F_MESHES) == 0) return pick5<C, F_MESHES>(need);
+      return pick5<C, F_ALL>(need);
   }
 }
 static uint32_t stack_lds(uint32_t feat, uint32_t need) {

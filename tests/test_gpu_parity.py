@@ -116,3 +116,13 @@ def test_path_kernel_times(gpu):
     t = s.path_kernel_times(0)
     assert len(t) == 2 and all(x > 0 for x in t)
     assert s.path_kernel_times(0) == []  # consumed
+
+
+@pytest.mark.parametrize("name,aspect,w,h,spp", [SCENES[1], SCENES[2], SCENES[3], SCENES[5]])
+def test_generic_kernel_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
+    """Every scene normally runs the smallest specialised kernel variant covering its features
+    (F_SPHERES / F_BOXES / F_MESHES, rtw_device.hpp); the all-features kernel must agree too."""
+    monkeypatch.setenv("RTW_GENERIC", "1")
+    g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
+    assert st["rays"] == rays
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
