@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
+#define RTW_ABI_VERSION 3
 
 enum {
   RTW_OK = 0,
@@ -85,6 +85,13 @@ int rtw_texture_solid(rtw_scene* s, float r, float g, float b, uint32_t* id);
 int rtw_texture_checker(rtw_scene* s, uint32_t odd, uint32_t even, float frequency, uint32_t* id);
 int rtw_texture_image(rtw_scene* s, const uint8_t* rgb8, uint32_t width, uint32_t height, uint32_t* id);
 int rtw_texture_uvdebug(rtw_scene* s, uint32_t* id);
+/* texture.rs:83-95 Noise::new(Perlin, scale): value = 0.5 (1 + sin(scale p.z + 10 turbulence(p, 7))).
+ * The Perlin tables (perlin.rs:8-48) cross as data: gradients 256x3 floats (unit vectors),
+ * permutations 3x256 (x, y, z; each a permutation of 0..255, else RTW_EINVAL).  Perlin::new(rng)
+ * with this build's seeded stream is rtw_perlin_generate(). */
+int rtw_texture_noise(rtw_scene* s, const float* gradients, const uint32_t* permutations, float scale,
+                      uint32_t* id);
+int rtw_perlin_generate(uint64_t seed, float* gradients, uint32_t* permutations);
 
 /* ---- materials: material.rs:30-39 Lambertian::new, :63-73 Metal::new (fuzz <= 1 else
  *      RTW_EINVAL, as the assert at :71), :102-105 Dielectric::new, light_source.rs:12-15
@@ -93,6 +100,8 @@ int rtw_material_lambertian(rtw_scene* s, uint32_t texture, uint32_t* id);
 int rtw_material_metal(rtw_scene* s, float r, float g, float b, float fuzz, uint32_t* id);
 int rtw_material_dielectric(rtw_scene* s, float index_of_refraction, uint32_t* id);
 int rtw_material_diffuse_light(rtw_scene* s, uint32_t texture, uint32_t* id);
+/* material.rs:148-165 Isotropic::new(albedo texture): scatters into random_in_unit_sphere */
+int rtw_material_isotropic(rtw_scene* s, uint32_t texture, uint32_t* id);
 
 /* ---- hierarchy.  Objects are appended to the innermost open group (the world list at the
  *      top).  Groups nest; each must be closed with rtw_end().
@@ -100,11 +109,18 @@ int rtw_material_diffuse_light(rtw_scene* s, uint32_t texture, uint32_t* id);
  *      rtw_begin_bvh:       BvhNode::new(objects, t0, t1, rng)  bvh.rs:19-74
  *      rtw_begin_translate: Translation::new(inner, offset)    transformations.rs:16-47
  *      rtw_begin_rotate_y:  YRotation::new(inner, degrees)     transformations.rs:50-75
+ *      rtw_begin_constant_medium: ConstantMedium::new(boundary, density, texture) volumes.rs:17-35;
+ *        the group holds the boundary: exactly one object, a Sphere or a Cuboid (optionally under
+ *        Translation / YRotation) in this build, else RTW_EINVAL at rtw_end / commit.  Creates the
+ *        medium's Isotropic(texture) phase function, whose id goes to *material (may be NULL).
+ *        The medium's free-path draw comes from a sub-stream keyed by (path segment, medium),
+ *        not the path's shared stream (order-independent form).
  *      A wrapper applies to everything added inside it (= the wrapper of a list). */
 int rtw_begin_list(rtw_scene* s);
 int rtw_begin_bvh(rtw_scene* s, float time0, float time1);
 int rtw_begin_translate(rtw_scene* s, float x, float y, float z);
 int rtw_begin_rotate_y(rtw_scene* s, float degrees);
+int rtw_begin_constant_medium(rtw_scene* s, float density, uint32_t texture, uint32_t* material);
 int rtw_end(rtw_scene* s);
 
 /* ---- primitives (SoA arrays of length n; copied)
@@ -180,15 +196,26 @@ int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* 
  * (Benchmark hook: the render call itself also enqueues the in-order sample reduction.) */
 int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
 
+/* Diagnostics: evaluate the render path's f32 transcendentals on the device over n host values
+ * (fn 0 log10f(a), 1 sinf(a), 2 acosf(a), 3 atan2f(a, b); DESIGN.md §Parity: correctly rounded).
+ * Used by the parity tests to pin the device functions against the oracle's. */
+int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
+
 /* console_app/src/main.rs:68-90 tonemap: sqrt(sum/spp), clamp [0, 0.999], u8(255.999*c). */
 int rtw_tonemap(const float* rgb_sum, uint32_t n_pixels, uint32_t spp, uint8_t* rgb8);
 
-/* ---- scene presets: console_app/src/scenes.rs restated (jumpy-balls :63-162,
- *      cornell-box :350-414, wavefront-cow-obj :719-771, textured-monument :816-858,
- *      two-spheres, simple-light, simple-triangle).  `seed` replaces thread_rng() for
- *      the random placement; models_dir holds the meshes.  Fills cam and background. */
+/* ---- scene presets: console_app/src/scenes.rs restated (jumpy-balls :63-162, two-spheres
+ *      :164-209, two-perlin-spheres :211-252, earth :254-288, simple-light :290-348, cornell-box
+ *      :350-414, smokey-cornell-box :416-483, book2-final-scene :485-620,
+ *      animated-book2-final-scene :622-667, simple-triangle :669-717, wavefront-cow-obj :719-771,
+ *      textured-monument :816-858).  `seed` replaces thread_rng() for the random placement;
+ *      models_dir holds the meshes and images.  Fills cam (the first camera) and background. */
 int rtw_scene_preset(rtw_scene* s, const char* name, float aspect_ratio, uint64_t seed,
                      const char* models_dir, rtw_camera* cam, float background[3]);
+/* All cameras of a preset (World = (objects, Vec<Camera>, background), scenes.rs:42-58):
+ * 30 for animated-book2-final-scene, 1 otherwise.  *n = the count; min(cap, *n) written. */
+int rtw_preset_cameras(const char* name, float aspect_ratio, const char* models_dir, rtw_camera* cams,
+                       uint32_t cap, uint32_t* n);
 
 /* Introspection for the test harness: the committed hierarchy as text (DESIGN.md
  * §Scene text).  Returns the required size (incl. NUL) in *needed; writes when cap
@@ -197,7 +224,7 @@ int rtw_scene_dump(const rtw_scene* s, char* buf, size_t cap, size_t* needed);
 int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32_t* w, uint32_t* h);
 /* 0 leaf primitives, 1 materials, 2 textures, 3 BVH nodes, 4 BVH depth, 5 always-tested
  * primitives, 6 instances, 7 BVH2 nodes, 8 traversal-stack bound, 9 feature mask (rtw_device.hpp
- * Feature; selects the path-kernel variant).  7-9 are valid once rtw_scene_commit has flattened
+ * Feature; selects the path-kernel variant), 10 Perlin tables.  7-9 are valid once rtw_scene_commit has flattened
  * the scene (also when its upload failed for lack of a device). */
 int64_t rtw_scene_info(const rtw_scene* s, int what);
 

@@ -65,6 +65,10 @@ def lib() -> C.CDLL:
             "oracle_get_ray": (None, [C.POINTER(oracle_camera), C.c_float, C.c_float, _U32, C.c_uint32, _F,
                                       _U32]),
             "oracle_tonemap": (C.c_uint8, [C.c_float, C.c_uint32]),
+            "oracle_libm": (C.c_int, [C.c_int, C.c_uint32, _F, _F, _F]),
+            "oracle_medium_hit": (C.c_int, [C.c_int, _F, C.c_float, _F, C.c_float, C.c_float, C.c_uint64,
+                                            C.c_uint32, _F]),
+            "oracle_noise": (C.c_float, [_F, C.POINTER(C.c_int32), _F, C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -131,3 +135,20 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(lib().oracle_last_error().decode())
         return out, int(rays.value)
+
+
+def libm(fn: int, a, b=None) -> np.ndarray:
+    """The oracle's f32 transcendentals (0 log10f, 1 sinf, 2 acosf, 3 atan2f(a, b))."""
+    a = f32(a)
+    bb = f32(b) if b is not None else None
+    out = np.empty_like(a)
+    if lib().oracle_libm(fn, len(a), fp(a), fp(bb) if bb is not None else None, fp(out)) != 0:
+        raise ValueError(fn)
+    return out
+
+
+def noise(grad, perm, p, depth: int = 7) -> float:
+    """perlin.rs noise (depth 0) / turbulence(p, depth) over explicit tables."""
+    g = f32(grad)
+    pm = np.ascontiguousarray(np.asarray(perm, np.int32).reshape(-1))
+    return float(lib().oracle_noise(fp(g), pm.ctypes.data_as(C.POINTER(C.c_int32)), fp(f32(p)), depth))

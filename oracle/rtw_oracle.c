@@ -153,6 +153,121 @@ static inline vec3 rand_in_unit_disk(draws* d) {
   }
 }
 
+
+/* ------------------------------------------------------------------ libm (f32 transcendentals)
+ * Rust's f32::sin / acos / atan2 / log10 call the platform libm.  glibc 2.35's float versions
+ * (this image) are faithfully but not correctly rounded (<= 1 ulp; e.g. log10f differs from the
+ * correctly rounded value for 23% of the rand Standard<f32> inputs), and other platforms' libms
+ * differ again, so the reference's exact bits are platform-defined.  This build defines them as
+ * the CORRECTLY ROUNDED values: each function is evaluated in double precision with a
+ * polynomial of error < 2^-60 and rounded once to f32.  Only IEEE double +,-,*,/,sqrt and floor
+ * are used (no FMA contraction), so the GPU kernel (rtw_kernel.hip, same algorithm) produces
+ * the same bits.  tests/test_libm.py pins these against (float)glibc-double exhaustively
+ * over the ranges the render path reaches; tests/test_gpu_parity.py pins GPU == oracle. */
+static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+/* ln(m), m in [sqrt(1/2), sqrt(2)]: 2 atanh(s), s = (m-1)/(m+1), |s| <= 0.1716 */
+static double ol_ln_core(double m) {
+  double s = (m - 1.0) / (m + 1.0), z = s * s;
+  double p = 1.0 / 23.0;
+  p = p * z + 1.0 / 21.0; p = p * z + 1.0 / 19.0; p = p * z + 1.0 / 17.0; p = p * z + 1.0 / 15.0;
+  p = p * z + 1.0 / 13.0; p = p * z + 1.0 / 11.0; p = p * z + 1.0 / 9.0; p = p * z + 1.0 / 7.0;
+  p = p * z + 1.0 / 5.0; p = p * z + 1.0 / 3.0; p = p * z + 1.0;
+  return 2.0 * s * p;
+}
+float oracle_log10f(float x) {
+  if (x != x) return x;
+  if (x == 0.0f) return -INFINITY;
+  if (x < 0.0f) return NAN;
+  if (isinf(x)) return x;
+  uint64_t u = d2u((double)x);
+  int e = (int)((u >> 52) & 0x7ff) - 1023; /* x normal or subnormal as f32 is normal as f64 */
+  double m = u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+  const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+  const double INV_LN10 = 0.43429448190325182765;
+  double lnx = ((double)e * LN2_HI + ol_ln_core(m)) + (double)e * LN2_LO;
+  return (float)(lnx * INV_LN10);
+}
+static double ol_sin_core(double r) { /* |r| <= pi/4 */
+  double z = r * r, p = -1.0 / 1307674368000.0;
+  p = p * z + 1.0 / 6227020800.0; p = p * z - 1.0 / 39916800.0; p = p * z + 1.0 / 362880.0;
+  p = p * z - 1.0 / 5040.0; p = p * z + 1.0 / 120.0; p = p * z - 1.0 / 6.0;
+  return r + r * z * p;
+}
+static double ol_cos_core(double r) {
+  double z = r * r, p = 1.0 / 20922789888000.0;
+  p = p * z - 1.0 / 87178291200.0; p = p * z + 1.0 / 479001600.0; p = p * z - 1.0 / 3628800.0;
+  p = p * z + 1.0 / 40320.0; p = p * z - 1.0 / 720.0; p = p * z + 1.0 / 24.0; p = p * z - 0.5;
+  return 1.0 + z * p;
+}
+float oracle_sinf(float x) {
+  if (x != x || x == 0.0f) return x; /* keeps the sign of zero */
+  if (isinf(x)) return NAN;
+  double d = x;
+  /* Cody-Waite reduction by pi/2 (three 33-bit parts: exact products for |k| < 2^20) */
+  const double TWO_OVER_PI = 6.36619772367581382433e-01;
+  const double P1 = 1.57079632673412561417e+00, P2 = 6.07710050650619224932e-11,
+               P3 = 2.02226624879595063154e-21;
+  double k = floor(d * TWO_OVER_PI + 0.5);
+  double r = ((d - k * P1) - k * P2) - k * P3;
+  double q = k - 4.0 * floor(k * 0.25);
+  double v = q == 0.0 ? ol_sin_core(r) : (q == 1.0 ? ol_cos_core(r) : (q == 2.0 ? -ol_sin_core(r) : -ol_cos_core(r)));
+  return (float)v;
+}
+static double ol_atan_core(double t) { /* |t| <= tan(pi/16) */
+  double z = t * t, p = -1.0 / 29.0;
+  p = p * z + 1.0 / 27.0; p = p * z - 1.0 / 25.0; p = p * z + 1.0 / 23.0; p = p * z - 1.0 / 21.0;
+  p = p * z + 1.0 / 19.0; p = p * z - 1.0 / 17.0; p = p * z + 1.0 / 15.0; p = p * z - 1.0 / 13.0;
+  p = p * z + 1.0 / 11.0; p = p * z - 1.0 / 9.0; p = p * z + 1.0 / 7.0; p = p * z - 1.0 / 5.0;
+  p = p * z + 1.0 / 3.0;
+  return t - t * z * p;
+}
+static double ol_atan01(double a) { /* 0 <= a <= 1: atan(a) = j pi/8 + atan((a - c_j) / (1 + a c_j)) */
+  const double T1 = 0.19891236737965800691, T3 = 0.66817863791929891999; /* tan(pi/16), tan(3pi/16) */
+  const double C1 = 0.41421356237309504880;                               /* tan(pi/8) */
+  const double PI_8 = 0.39269908169872415481, PI_4 = 0.78539816339744830962;
+  if (a <= T1) return ol_atan_core(a);
+  if (a <= T3) return PI_8 + ol_atan_core((a - C1) / (1.0 + a * C1));
+  return PI_4 + ol_atan_core((a - 1.0) / (1.0 + a));
+}
+static double ol_atan2_pos(double y, double x) { /* y > 0 finite, x finite non-zero */
+  const double PI = 3.14159265358979323846, PI_2 = 1.57079632679489661923;
+  double ax = fabs(x), r;
+  r = y <= ax ? ol_atan01(y / ax) : PI_2 - ol_atan01(ax / y);
+  return x < 0.0 ? PI - r : r;
+}
+float oracle_atan2f(float y, float x) { /* C99 Annex F special cases, as glibc */
+  const double PI = 3.14159265358979323846, PI_2 = 1.57079632679489661923, PI_4 = 0.78539816339744830962;
+  if (x != x || y != y) return x + y;
+  const int sx = signbit(x) != 0, sy = signbit(y) != 0;
+  double r;
+  if (y == 0.0f) r = sx ? PI : 0.0;
+  else if (isinf(x)) r = isinf(y) ? (sx ? 3.0 * PI_4 : PI_4) : (sx ? PI : 0.0);
+  else if (x == 0.0f || isinf(y)) r = PI_2;
+  else r = ol_atan2_pos(fabs((double)y), (double)x);
+  return (float)(sy ? -r : r);
+}
+float oracle_acosf(float x) { /* acos x = atan2(sqrt((1-x)(1+x)), x); (1-x)(1+x) is exact in f64 */
+  if (x != x) return x;
+  if (!(fabsf(x) <= 1.0f)) return NAN;
+  double d = x, s = sqrt((1.0 - d) * (1.0 + d));
+  if (s == 0.0) return d > 0.0 ? 0.0f : (float)3.14159265358979323846;
+  return (float)ol_atan2_pos(s, d);
+}
+int oracle_libm(int fn, uint32_t n, const float* a, const float* b, float* out) {
+  for (uint32_t k = 0; k < n; ++k) {
+    switch (fn) {
+      case 0: out[k] = oracle_log10f(a[k]); break;
+      case 1: out[k] = oracle_sinf(a[k]); break;
+      case 2: out[k] = oracle_acosf(a[k]); break;
+      case 3: out[k] = oracle_atan2f(a[k], b[k]); break;
+      default: return -22;
+    }
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------ ray.rs */
 typedef struct { vec3 o, d; float time; } ray;
 static inline vec3 ray_at(const ray* r, float t) { return vadd(r->o, vscale(r->d, t)); } /* ray.rs:25-27 */
@@ -197,15 +312,18 @@ static ray camera_get_ray(const oracle_camera* c, float s, float t, draws* d) {
 }
 
 /* ------------------------------------------------------------------ scene model */
-enum { T_SOLID, T_CHECKER, T_IMAGE, T_UVDEBUG };
-typedef struct { int kind; float c[3]; int odd, even; float freq; int w, h; const uint8_t* img; } otex;
-enum { M_LAMBERT, M_METAL, M_DIELECTRIC, M_LIGHT };
+enum { T_SOLID, T_CHECKER, T_IMAGE, T_UVDEBUG, T_NOISE };
+/* perlin.rs:8-12: 256 gradients, three permutations */
+typedef struct { vec3 g[256]; int perm[3][256]; } operlin;
+typedef struct { int kind; float c[3]; int odd, even; float freq; int w, h; const uint8_t* img; operlin* perlin; } otex;
+enum { M_LAMBERT, M_METAL, M_DIELECTRIC, M_LIGHT, M_ISOTROPIC };
 typedef struct { int kind; int tex; float albedo[3]; float fuzz; float ir; } omat;
 
-enum { K_LIST, K_BVH, K_TRANSLATE, K_ROTY, K_SPHERE, K_MSPHERE, K_RECT, K_CUBOID, K_TRI, K_BVHNODE };
+enum { K_LIST, K_BVH, K_TRANSLATE, K_ROTY, K_SPHERE, K_MSPHERE, K_RECT, K_CUBOID, K_TRI, K_BVHNODE, K_MEDIUM };
 typedef struct { vec3 mn, mx; int ok; } aabb;
 typedef struct onode {
   int kind, mat, axis;
+  uint32_t key;        /* DFS leaf index (world leaves; a ConstantMedium is one leaf) */
   int n, cap;
   struct onode** ch;
   float f[16];         /* primitive / wrapper parameters */
@@ -259,8 +377,8 @@ static aabb surrounding(aabb a, aabb b) { /* aabb.rs:74-88 */
 void oracle_sphere_uv(const float p[3], float uv[2]) {
   /* spherical.rs:62-77 */
   const float PI = 3.14159265358979323846f;
-  float theta = acosf(-p[1]);
-  float phi = atan2f(-p[2], p[0]) + PI;
+  float theta = oracle_acosf(-p[1]);         /* f32::acos / atan2: correctly rounded, see libm */
+  float phi = oracle_atan2f(-p[2], p[0]) + PI;
   uv[0] = phi / (2.0f * PI);
   uv[1] = theta / PI;
 }
@@ -343,6 +461,9 @@ static int hit_tri(const onode* tr, const ray* r, float tmin, float tmax, hitrec
 }
 
 static int node_hit(const onode* nd, const ray* r, float tmin, float tmax, int bvh_mode, hitrec* h);
+/* The path's RNG state at the start of the current segment (set by world_hit): keys the
+ * ConstantMedium draw, see K_MEDIUM below. */
+static __thread uint64_t g_seg;
 
 /* hittable/mod.rs:57-69 — linear closest hit, later object wins exact ties */
 static int list_hit(onode* const* ch, int n, const ray* r, float tmin, float tmax, int bvh_mode,
@@ -411,6 +532,37 @@ static int node_hit(const onode* nd, const ray* r, float tmin, float tmax, int b
       return hit_rect(r, tmin, tmax, nd->axis, nd->f, nd->mat, h);
     case K_TRI:
       return hit_tri(nd, r, tmin, tmax, h);
+    case K_MEDIUM: { /* volumes.rs:37-78 */
+      hitrec r1, r2;
+      if (nd->n != 1) return 0;
+      if (!node_hit(nd->ch[0], r, -INFINITY, INFINITY, bvh_mode, &r1)) return 0;
+      if (!node_hit(nd->ch[0], r, r1.t + 0.0001f, INFINITY, bvh_mode, &r2)) return 0;
+      float t1 = fmaxf(r1.t, tmin); /* f32::max ignores NaN = fmaxf */
+      /* Deviation: the reference clips rec2 to t_max (the closest hit so far)
+       * and draws from the path's shared stream only when the clipped interval is non-empty, so
+       * its draws depend on the order objects are tested in.  Here the distance test uses the
+       * unclipped rec2 and the draw comes from a sub-stream keyed by (segment state, leaf key);
+       * the candidate t is then compared with t_max like any primitive's, which makes the
+       * answer independent of traversal order (the GPU's BVH order reproduces it). */
+      float t2 = r2.t;
+      if (t1 >= t2) return 0;
+      t1 = fmaxf(t1, 0.0f);
+      float len = sqrtf(vlen2(r->d)); /* vec3.rs:81-83 */
+      float dist = (t2 - t1) * len;
+      pcg32 g = {oracle_splitmix64(g_seg ^ oracle_splitmix64((uint64_t)nd->key))};
+      float hd = nd->f[1] * oracle_log10f(oracle_u32_to_f32(pcg_next(&g)));
+      if (hd > dist) return 0;
+      float t = t1 + hd / len;
+      if (t > tmax) return 0;
+      h->t = t;
+      h->p = ray_at(r, t);
+      h->n = v3(1.0f, 0.0f, 0.0f); /* arbitrary (volumes.rs:65-66) */
+      h->front = 1;
+      h->u = 0.0f;
+      h->v = 0.0f;
+      h->mat = nd->mat;
+      return 1;
+    }
   }
   return 0;
 }
@@ -473,6 +625,8 @@ static aabb node_box(const onode* nd, float t0, float t1) {
     }
     case K_ROTY:
       return nd->rot_box;
+    case K_MEDIUM: /* volumes.rs:80-82 */
+      return nd->n == 1 ? node_box(nd->ch[0], t0, t1) : b;
     case K_BVHNODE:
       return nd->box;
     case K_LIST:
@@ -553,6 +707,60 @@ static onode* build_ref_bvh(onode** objs, int n, float t0, float t1, pcg32* rng)
 }
 
 /* ------------------------------------------------------------------ textures / materials */
+/* perlin.rs:50-76 noise: lattice corners hashed by permutation xor, trilinear blend (perlin_interp
+ * :93-117 — the Hermite-filtered point is used for both the blend and the weight vector, as the
+ * reference's shadowing `let point_within_lattice_cell = filter_hermit(..)` makes it) */
+static int64_t f32_as_i64(float x) { /* Rust `as i64`: saturating, NaN -> 0 */
+  if (x != x) return 0;
+  if (x >= 9223372036854775807.0f) return INT64_MAX;
+  if (x <= -9223372036854775808.0f) return INT64_MIN;
+  return (int64_t)x;
+}
+static float perlin_noise(const operlin* P, vec3 p) {
+  vec3 fl = v3(floorf(p.x), floorf(p.y), floorf(p.z));
+  uint64_t base[3] = {(uint64_t)f32_as_i64(fl.x), (uint64_t)f32_as_i64(fl.y), (uint64_t)f32_as_i64(fl.z)};
+  vec3 w = vsub(p, fl);
+  vec3 g[2][2][2];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int k = 0; k < 2; ++k) {
+        int hash = P->perm[0][(base[0] + (uint64_t)i) & 255] ^ P->perm[1][(base[1] + (uint64_t)j) & 255] ^
+                   P->perm[2][(base[2] + (uint64_t)k) & 255];
+        g[i][j][k] = P->g[hash];
+      }
+  vec3 f = vmul(vmul(w, w), vsub(v3(3.0f, 3.0f, 3.0f), vscale(w, 2.0f))); /* filter_hermit :119-122 */
+  const vec3 one = v3(1.0f, 1.0f, 1.0f);
+  float accum = 0.0f;
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int k = 0; k < 2; ++k) {
+        vec3 c = v3((float)i, (float)j, (float)k);
+        vec3 wv = vsub(f, c);
+        vec3 bl = vadd(vmul(c, f), vmul(vsub(one, c), vsub(one, f)));
+        float bf = bl.x * bl.y * bl.z; /* vec3.rs:58-62 internal_product */
+        accum += bf * vdot(g[i][j][k], wv);
+      }
+  return accum;
+}
+static float perlin_turbulence(const operlin* P, vec3 p, int depth) { /* perlin.rs:78-91 */
+  float accum = 0.0f, weight = 1.0f;
+  vec3 tp = p;
+  for (int d = 0; d < depth; ++d) {
+    accum += weight * perlin_noise(P, tp);
+    weight *= 0.5f;
+    tp = vscale(tp, 2.0f);
+  }
+  return fabsf(accum);
+}
+float oracle_noise(const float* grad, const int32_t* perm, const float p[3], int depth) {
+  operlin P;
+  for (int k = 0; k < 256; ++k) {
+    P.g[k] = v3(grad[3 * k], grad[3 * k + 1], grad[3 * k + 2]);
+    for (int a = 0; a < 3; ++a) P.perm[a][k] = perm[256 * a + k];
+  }
+  return depth <= 0 ? perlin_noise(&P, v3(p[0], p[1], p[2])) : perlin_turbulence(&P, v3(p[0], p[1], p[2]), depth);
+}
+
 /* texture.rs:56-60 SolidColor, :69-81 Checker, image_texture.rs:34-52 ImageTexture, texture.rs:97-104 UVDebug */
 static vec3 tex_value(const oracle_scene* s, int id, float u, float v, vec3 p) {
   for (;;) {
@@ -578,6 +786,11 @@ static vec3 tex_value(const oracle_scene* s, int id, float u, float v, vec3 p) {
         return v3((float)px[0] * scale, (float)px[1] * scale, (float)px[2] * scale);
       }
       case T_UVDEBUG: return v3(u, v, 0.0f);
+      case T_NOISE: { /* texture.rs:89-95: Color(1,1,1) * 0.5 * (1 + sin(scale z + 10 turb(p, 7))) */
+        float tb = perlin_turbulence(t->perlin, p, 7);
+        float sv = 0.5f * (1.0f + oracle_sinf(t->freq * p.z + 10.0f * tb));
+        return v3(sv, sv, sv);
+      }
     }
     return v3(0, 0, 0);
   }
@@ -627,6 +840,10 @@ static int mat_scatter(const oracle_scene* s, const omat* m, const ray* rin, con
     }
     case M_LIGHT: /* light_source.rs:18-20 */
       return 0;
+    case M_ISOTROPIC: /* material.rs:155-165: random_in_unit_sphere direction, never absorbs */
+      out->att = tex_value(s, m->tex, h->u, h->v, h->p);
+      out->out.o = h->p; out->out.d = rand_in_unit_sphere(d); out->out.time = rin->time;
+      return 1;
   }
   return 0;
 }
@@ -643,15 +860,16 @@ typedef struct {
   uint64_t rays;
 } ctx_t;
 
-static int world_hit(ctx_t* c, const ray* r, hitrec* h) {
+static int world_hit(ctx_t* c, const ray* r, const draws* d, hitrec* h) {
   c->rays++;
+  g_seg = d->rng.s;
   return list_hit(c->s->root->ch, c->s->root->n, r, 0.001f, INFINITY, c->bvh_mode, h); /* lib.rs:102 */
 }
 /* lib.rs:97-117, literal recursion: emitted + attenuation * sample_ray(next) */
 static vec3 sample_ray_rec(ctx_t* c, const ray* r, draws* d, uint32_t depth) {
   if (depth == 0) return v3(0, 0, 0);
   hitrec h;
-  if (!world_hit(c, r, &h)) return c->bg;
+  if (!world_hit(c, r, d, &h)) return c->bg;
   const omat* m = &c->s->mat[h.mat];
   vec3 e = mat_emitted(c->s, m, &h);
   scatter_t sc;
@@ -665,7 +883,7 @@ static vec3 sample_ray_iter(ctx_t* c, ray r, draws* d, uint32_t depth) {
   vec3 T = v3(1.0f, 1.0f, 1.0f);
   for (; depth > 0; --depth) {
     hitrec h;
-    if (!world_hit(c, &r, &h)) return vmul(T, c->bg);
+    if (!world_hit(c, &r, d, &h)) return vmul(T, c->bg);
     const omat* m = &c->s->mat[h.mat];
     scatter_t sc;
     if (!mat_scatter(c->s, m, &r, &h, d, &sc)) return vmul(T, mat_emitted(c->s, m, &h));
@@ -771,6 +989,7 @@ static void free_node(onode* n) {
 void oracle_scene_free(oracle_scene* s) {
   if (!s) return;
   free_node(s->root);
+  for (int k = 0; k < s->ntex; ++k) free(s->tex[k].perlin);
   free(s->tex);
   free(s->mat);
   free(s);
@@ -833,6 +1052,13 @@ static void prepare(onode* n, oracle_scene* s, pcg32* rng) {
   }
 }
 
+/* a primitive of the world gets the next DFS leaf key; inside a ConstantMedium it is boundary
+ * geometry, not a world leaf */
+static void add_leaf(oracle_scene* s, onode* parent, onode* n, int medium_depth) {
+  if (medium_depth == 0) n->key = (uint32_t)s->nleaf++;
+  add_child(parent, n);
+}
+
 oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images, int n_images) {
   oracle_scene* s = (oracle_scene*)calloc(1, sizeof(oracle_scene));
   s->root = new_node(K_LIST);
@@ -841,7 +1067,7 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
   stack[sp] = s->root;
   lexer L = {text};
   char tok[64];
-  int line = 0, ok = 1;
+  int line = 0, ok = 1, medium_depth = 0;
   uint64_t bvh_seed = 0;
   while (*L.p && ok) {
     line++;
@@ -872,7 +1098,20 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
             ok = tok_i(&L, &b) && tok_i(&L, &c) && tok_i(&L, &d) && d >= 0 && d < n_images && b > 0 && c > 0;
             if (ok) { t->w = (int)b; t->h = (int)c; t->img = images[d]; }
           } else if (!strcmp(kind, "uvdebug")) { t->kind = T_UVDEBUG; }
-          else ok = 0;
+          else if (!strcmp(kind, "noise")) { /* texture.rs:83-87 Noise{noise: Perlin, scale} */
+            t->kind = T_NOISE;
+            t->perlin = (operlin*)calloc(1, sizeof(operlin));
+            ok = tok_f(&L, &t->freq);
+            for (int k = 0; ok && k < 256; ++k) {
+              float g3[3];
+              ok = tok_fn(&L, g3, 3);
+              t->perlin->g[k] = v3(g3[0], g3[1], g3[2]);
+            }
+            for (int k = 0; ok && k < 768; ++k) {
+              ok = tok_i(&L, &b) && b >= 0 && b < 256;
+              t->perlin->perm[k / 256][k % 256] = (int)b;
+            }
+          } else ok = 0;
           s->ntex++;
         }
       } else if (!strcmp(tok, "mat")) {
@@ -886,6 +1125,7 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
           else if (!strcmp(kind, "metal")) { m->kind = M_METAL; ok = tok_fn(&L, m->albedo, 3) && tok_f(&L, &m->fuzz); }
           else if (!strcmp(kind, "dielectric")) { m->kind = M_DIELECTRIC; ok = tok_f(&L, &m->ir); }
           else if (!strcmp(kind, "light")) { m->kind = M_LIGHT; ok = tok_i(&L, &b); m->tex = (int)b; ok = ok && b < s->ntex; }
+          else if (!strcmp(kind, "isotropic")) { m->kind = M_ISOTROPIC; ok = tok_i(&L, &b); m->tex = (int)b; ok = ok && b < s->ntex; }
           else ok = 0;
           s->nmat++;
         }
@@ -903,22 +1143,29 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
             float rad = to_radians(n->f[0]); /* transformations.rs:60-63 */
             n->sin_t = sinf(rad);
             n->cos_t = cosf(rad);
+          } else if (!strcmp(kind, "medium")) { /* volumes.rs:24-35 ConstantMedium::new */
+            n = new_node(K_MEDIUM);
+            ok = tok_f(&L, &n->f[0]) && tok_i(&L, &a) && a < s->nmat;
+            n->f[1] = -1.0f / n->f[0]; /* neg_inv_density */
+            n->mat = (int)a;
+            if (ok && medium_depth == 0) n->key = (uint32_t)s->nleaf++;
           } else ok = 0;
         }
-        if (ok) { add_child(stack[sp], n); stack[++sp] = n; }
+        if (ok) { add_child(stack[sp], n); stack[++sp] = n; if (n->kind == K_MEDIUM) medium_depth++; }
       } else if (!strcmp(tok, "end")) {
         ok = sp > 0;
+        if (ok && stack[sp]->kind == K_MEDIUM) { medium_depth--; ok = stack[sp]->n == 1; }
         sp--;
       } else if (!strcmp(tok, "sphere")) {
         onode* n = new_node(K_SPHERE);
         ok = tok_fn(&L, n->f, 4) && tok_i(&L, &a) && a < s->nmat;
         n->mat = (int)a;
-        add_child(stack[sp], n); s->nleaf++;
+        add_leaf(s, stack[sp], n, medium_depth);
       } else if (!strcmp(tok, "msphere")) {
         onode* n = new_node(K_MSPHERE);
         ok = tok_fn(&L, n->f, 9) && tok_i(&L, &a) && a < s->nmat;
         n->mat = (int)a;
-        add_child(stack[sp], n); s->nleaf++;
+        add_leaf(s, stack[sp], n, medium_depth);
       } else if (!strcmp(tok, "rect")) {
         char ax[8];
         onode* n = new_node(K_RECT);
@@ -926,7 +1173,7 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
         n->axis = !strcmp(ax, "xy") ? 0 : (!strcmp(ax, "xz") ? 1 : (!strcmp(ax, "yz") ? 2 : -1));
         ok = ok && n->axis >= 0;
         n->mat = (int)a;
-        add_child(stack[sp], n); s->nleaf++;
+        add_leaf(s, stack[sp], n, medium_depth);
       } else if (!strcmp(tok, "cuboid")) {
         /* rectangular.rs:177-234: six sides in this order */
         onode* n = new_node(K_CUBOID);
@@ -943,9 +1190,9 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
           r->axis = (int)sides[k][0];
           for (int q = 0; q < 5; ++q) r->f[q] = sides[k][q + 1];
           r->mat = (int)a;
-          add_child(n, r);
+          add_leaf(s, n, r, medium_depth);
         }
-        add_child(stack[sp], n); s->nleaf += 6;
+        add_child(stack[sp], n);
       } else if (!strcmp(tok, "tri")) {
         /* triangular.rs:42-73: missing normals -> geometric normal, missing uv -> defaults */
         onode* n = new_node(K_TRI);
@@ -962,7 +1209,7 @@ oracle_scene* oracle_scene_parse(const char* text, const uint8_t* const* images,
           n->tuv[k][1] = (uvmask >> k) & 1 ? uv[2 * k + 1] : defuv[k][1];
         }
         n->mat = (int)a;
-        add_child(stack[sp], n); s->nleaf++;
+        add_leaf(s, stack[sp], n, medium_depth);
       } else {
         ok = 0;
       }
@@ -1021,7 +1268,7 @@ int oracle_scatter(int kind, const float* params, const float rr[7], const float
                    const uint32_t* arr, uint32_t n_draws, float* out, uint32_t* used) {
   oracle_scene s;
   memset(&s, 0, sizeof s);
-  otex t = {T_SOLID, {params[0], params[1], params[2]}, 0, 0, 0, 0, 0, NULL};
+  otex t = {T_SOLID, {params[0], params[1], params[2]}, 0, 0, 0, 0, 0, NULL, NULL};
   s.tex = &t; s.ntex = 1;
   omat m;
   memset(&m, 0, sizeof m);
@@ -1063,4 +1310,48 @@ uint8_t oracle_tonemap(float sum, uint32_t spp) {
   if (x != x || x <= 0.0f) return 0; /* `as u8` saturates, NaN -> 0 */
   if (x >= 255.0f) return 255;
   return (uint8_t)x;
+}
+
+/* ConstantMedium::hit (volumes.rs:37-78, order-independent form) around a Sphere (kind 0,
+ * params cx cy cz r) or a Cuboid (kind 1, p0[3] p1[3]) with the segment state `seg` and leaf
+ * key `key`; returns 1 and *t_out on a hit */
+int oracle_medium_hit(int kind, const float* params, float density, const float rr[7], float tmin, float tmax,
+                      uint64_t seg, uint32_t key, float* t_out) {
+  onode b, sides[6], med;
+  onode* side_ptr[6];
+  onode* bptr = &b;
+  memset(&b, 0, sizeof b);
+  memset(&med, 0, sizeof med);
+  if (kind == 0) {
+    b.kind = K_SPHERE;
+    memcpy(b.f, params, 4 * sizeof(float));
+  } else {
+    const float* p0 = params;
+    const float* p1 = params + 3;
+    const float sd[6][6] = {{0, p0[0], p1[0], p0[1], p1[1], p1[2]}, {0, p0[0], p1[0], p0[1], p1[1], p0[2]},
+                            {1, p0[0], p1[0], p0[2], p1[2], p1[1]}, {1, p0[0], p1[0], p0[2], p1[2], p0[1]},
+                            {2, p0[1], p1[1], p0[2], p1[2], p1[0]}, {2, p0[1], p1[1], p0[2], p1[2], p0[0]}};
+    b.kind = K_CUBOID;
+    for (int k = 0; k < 6; ++k) {
+      memset(&sides[k], 0, sizeof sides[k]);
+      sides[k].kind = K_RECT;
+      sides[k].axis = (int)sd[k][0];
+      for (int q = 0; q < 5; ++q) sides[k].f[q] = sd[k][q + 1];
+      side_ptr[k] = &sides[k];
+    }
+    b.ch = side_ptr;
+    b.n = 6;
+  }
+  med.kind = K_MEDIUM;
+  med.ch = &bptr;
+  med.n = 1;
+  med.f[0] = density;
+  med.f[1] = -1.0f / density;
+  med.key = key;
+  g_seg = seg;
+  ray r = ray_from(rr);
+  hitrec h;
+  if (!node_hit(&med, &r, tmin, tmax, ORACLE_BVH_AS_LIST, &h)) return 0;
+  *t_out = h.t;
+  return 1;
 }

@@ -78,6 +78,19 @@ int oracle_scatter(int kind, const float* params, const float ray[7], const floa
 void oracle_get_ray(const oracle_camera* cam, float s, float t, const uint32_t* draws,
                     uint32_t n_draws, float ray_out[7], uint32_t* used);
 uint8_t oracle_tonemap(float sum, uint32_t spp);
+/* f32 transcendentals as this build defines them (correctly rounded; rtw_oracle.c §libm):
+ * fn 0 log10f(a), 1 sinf(a), 2 acosf(a), 3 atan2f(a, b) over n values */
+int oracle_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
+float oracle_log10f(float x);
+float oracle_sinf(float x);
+float oracle_acosf(float x);
+float oracle_atan2f(float y, float x);
+/* ConstantMedium around a Sphere (kind 0: c[3], r) or Cuboid (kind 1: p0[3], p1[3]); seg = path
+ * RNG state at the segment start, key = the medium's DFS leaf key; 1 + *t_out on a hit */
+int oracle_medium_hit(int kind, const float* params, float density, const float ray[7], float tmin,
+                      float tmax, uint64_t seg, uint32_t key, float* t_out);
+/* perlin.rs noise (depth <= 0) or turbulence(p, depth); grad: 256x3, perm: 3x256 */
+float oracle_noise(const float* grad, const int32_t* perm, const float p[3], int depth);
 
 #ifdef __cplusplus
 }

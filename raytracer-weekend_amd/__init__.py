@@ -78,6 +78,9 @@ _SIGS = {
     "rtw_texture_checker": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, _U32]),
     "rtw_texture_image": (C.c_int, [C.c_void_p, _U8, C.c_uint32, C.c_uint32, _U32]),
     "rtw_texture_uvdebug": (C.c_int, [C.c_void_p, _U32]),
+    "rtw_texture_noise": (C.c_int, [C.c_void_p, _F, _U32, C.c_float, _U32]),
+    "rtw_perlin_generate": (C.c_int, [C.c_uint64, _F, _U32]),
+    "rtw_material_isotropic": (C.c_int, [C.c_void_p, C.c_uint32, _U32]),
     "rtw_material_lambertian": (C.c_int, [C.c_void_p, C.c_uint32, _U32]),
     "rtw_material_metal": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float, _U32]),
     "rtw_material_dielectric": (C.c_int, [C.c_void_p, C.c_float, _U32]),
@@ -86,6 +89,7 @@ _SIGS = {
     "rtw_begin_bvh": (C.c_int, [C.c_void_p, C.c_float, C.c_float]),
     "rtw_begin_translate": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float]),
     "rtw_begin_rotate_y": (C.c_int, [C.c_void_p, C.c_float]),
+    "rtw_begin_constant_medium": (C.c_int, [C.c_void_p, C.c_float, C.c_uint32, _U32]),
     "rtw_end": (C.c_int, [C.c_void_p]),
     "rtw_add_spheres": (C.c_int, [C.c_void_p, C.c_uint32, _F, _F, _F, _F, _U32]),
     "rtw_add_moving_spheres": (C.c_int, [C.c_void_p, C.c_uint32] + [_F] * 9 + [_U32]),
@@ -105,8 +109,11 @@ _SIGS = {
     "rtw_unpack_tiles_device": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
+    "rtw_diag_libm": (C.c_int, [C.c_int, C.c_uint32, _F, _F, _F]),
     "rtw_scene_preset": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_uint64, C.c_char_p,
                                    C.POINTER(rtw_camera), _F]),
+    "rtw_preset_cameras": (C.c_int, [C.c_char_p, C.c_float, C.c_char_p, C.POINTER(rtw_camera), C.c_uint32,
+                                     _U32]),
     "rtw_scene_dump": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rtw_scene_image": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(_U8), _U32, _U32]),
     "rtw_scene_info": (C.c_int64, [C.c_void_p, C.c_int]),
@@ -116,7 +123,7 @@ EXPORTED_SYMBOLS = tuple(_SIGS)
 _lib = None
 
 
-ABI_VERSION = 2  # include/rtw.h RTW_ABI_VERSION
+ABI_VERSION = 3  # include/rtw.h RTW_ABI_VERSION
 
 
 def lib() -> C.CDLL:
@@ -222,6 +229,13 @@ class Scene:
     def uv_debug(self) -> int:
         return self._id(lib().rtw_texture_uvdebug)
 
+    def noise(self, scale: float, perlin=None, seed: int = 0) -> int:
+        """Noise::new(Perlin, scale) (texture.rs:83-95).  perlin = (gradients[256, 3],
+        permutations[3, 256]); default Perlin::new with the build's seeded stream."""
+        g, p = perlin if perlin is not None else perlin_generate(seed)
+        g, p = _fa(g), _ua(p)
+        return self._id(lib().rtw_texture_noise, _fp(g), _up(p), float(scale))
+
     # materials -----------------------------------------------------------
     def lambertian(self, tex: int) -> int:
         return self._id(lib().rtw_material_lambertian, tex)
@@ -237,6 +251,9 @@ class Scene:
 
     def diffuse_light(self, tex: int) -> int:
         return self._id(lib().rtw_material_diffuse_light, tex)
+
+    def isotropic(self, tex: int) -> int:
+        return self._id(lib().rtw_material_isotropic, tex)
 
     # hierarchy -----------------------------------------------------------
     @contextlib.contextmanager
@@ -256,6 +273,11 @@ class Scene:
 
     def rotate_y(self, degrees):
         return self._group(lib().rtw_begin_rotate_y(self._p, float(degrees)))
+
+    def constant_medium(self, density: float, tex: int):
+        """ConstantMedium::new(boundary, density, texture) (volumes.rs:24-35): add the boundary
+        (one Sphere or Cuboid, optionally translated / rotated) inside the `with` block."""
+        return self._group(lib().rtw_begin_constant_medium(self._p, float(density), tex, None))
 
     # primitives ----------------------------------------------------------
     def spheres(self, centers, radii, mats) -> None:
@@ -384,9 +406,36 @@ class Raytracer:
         return st.as_dict() if want_stats else None
 
 
+def perlin_generate(seed: int = 0):
+    """Perlin::new(rng) (perlin.rs:14-48) with the build's seeded stream -> (grad[256, 3], perm[3, 256])."""
+    g = np.zeros(768, np.float32)
+    p = np.zeros(768, np.uint32)
+    _check(lib().rtw_perlin_generate(seed, _fp(g), _up(p)))
+    return g.reshape(256, 3), p.reshape(3, 256)
+
+
+def preset_cameras(name: str, aspect: float, models_dir=None) -> list:
+    """Every camera of a preset (scenes.rs World's Vec<Camera>): 30 for animated-book2-final-scene."""
+    n = C.c_uint32()
+    md = str(models_dir or MODELS_DIR).encode()
+    _check(lib().rtw_preset_cameras(name.encode(), aspect, md, None, 0, C.byref(n)))
+    cams = (rtw_camera * max(1, n.value))()
+    _check(lib().rtw_preset_cameras(name.encode(), aspect, md, cams, n.value, C.byref(n)))
+    return [Camera(cams[k]) for k in range(n.value)]
+
+
 def unpack_tiles_device(w, h, d_tiles_ptr, n_tiles, d_packed_ptr, d_image_ptr, device=-1, stream_ptr=0):
     _check(lib().rtw_unpack_tiles_device(device, w, h, C.c_void_p(d_tiles_ptr), n_tiles, C.c_void_p(d_packed_ptr),
                                          C.c_void_p(d_image_ptr), C.c_void_p(stream_ptr)))
+
+
+def diag_libm(fn: int, a, b=None) -> np.ndarray:
+    """Device f32 transcendentals (0 log10f, 1 sinf, 2 acosf, 3 atan2f(a, b)) over host arrays."""
+    a = _fa(a)
+    bb = _fa(b) if b is not None else None
+    out = np.empty_like(a)
+    _check(lib().rtw_diag_libm(fn, len(a), _fp(a), _fp(bb) if bb is not None else None, _fp(out)))
+    return out
 
 
 def n_tiles(w: int, h: int) -> int:

@@ -8,6 +8,7 @@
 
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/rtw.h"
 #include "rtw_scene.hpp"
@@ -53,8 +54,15 @@ static void dump_node(const Scene& s, uint32_t id, std::string& o) {
     case NK_LIST:
     case NK_BVH:
     case NK_TRANSLATE:
-    case NK_ROTY: {
+    case NK_ROTY:
+    case NK_MEDIUM: {
       if (n.kind == NK_LIST) o += "begin list";
+      else if (n.kind == NK_MEDIUM) {
+        o += "begin medium";
+        put_f(o, n.f[0]);
+        snprintf(b, sizeof b, " %u", n.mat);
+        o += b;
+      }
       else if (n.kind == NK_BVH) { o += "begin bvh"; put_f(o, n.f[0]); put_f(o, n.f[1]); }
       else if (n.kind == NK_TRANSLATE) { o += "begin translate"; for (int k = 0; k < 3; ++k) put_f(o, n.f[k]); }
       else { o += "begin rotate_y"; put_f(o, n.f[0]); }
@@ -109,7 +117,12 @@ std::string dump_scene(const Scene& s) {
     if (t.type == TT_SOLID) { o += "solid"; for (int c = 0; c < 3; ++c) put_f(o, t.c[c]); }
     else if (t.type == TT_CHECKER) { snprintf(b, sizeof b, "checker %u %u", t.odd, t.even); o += b; put_f(o, t.freq); }
     else if (t.type == TT_IMAGE) { snprintf(b, sizeof b, "image %u %u %u", t.w, t.h, img++); o += b; }
-    else o += "uvdebug";
+    else if (t.type == TT_NOISE) {
+      o += "noise";
+      put_f(o, t.freq);
+      for (float g : t.grad) put_f(o, g);
+      for (uint32_t q : t.perm) { snprintf(b, sizeof b, " %u", q); o += b; }
+    } else o += "uvdebug";
     o += "\n";
   }
   for (size_t k = 0; k < s.mat.size(); ++k) {
@@ -119,6 +132,7 @@ std::string dump_scene(const Scene& s) {
     if (m.type == MT_LAMBERT) { snprintf(b, sizeof b, "lambertian %u", m.tex); o += b; }
     else if (m.type == MT_METAL) { o += "metal"; for (int c = 0; c < 3; ++c) put_f(o, m.albedo[c]); put_f(o, m.param); }
     else if (m.type == MT_DIELECTRIC) { o += "dielectric"; put_f(o, m.param); }
+    else if (m.type == MT_ISOTROPIC) { snprintf(b, sizeof b, "isotropic %u", m.tex); o += b; }
     else { snprintf(b, sizeof b, "light %u", m.tex); o += b; }
     o += "\n";
   }
@@ -180,6 +194,23 @@ int rtw_texture_uvdebug(rtw_scene* s, uint32_t* id) {
   t.type = TT_UVDEBUG;
   return push_tex(s, std::move(t), id);
 }
+int rtw_texture_noise(rtw_scene* s, const float* grad, const uint32_t* perm, float scale, uint32_t* id) {
+  if (!grad || !perm) return fail(RTW_EINVAL, "noise texture needs 256x3 gradients and 3x256 permutations");
+  for (int a = 0; a < 3; ++a) {  // perlin.rs:30-48 builds permutations of 0..255; the hash indexes by them
+    bool seen[256] = {};
+    for (int k = 0; k < 256; ++k) {
+      const uint32_t v = perm[256 * a + k];
+      if (v > 255 || seen[v]) return fail(RTW_EINVAL, "noise permutation %d is not a permutation of 0..255", a);
+      seen[v] = true;
+    }
+  }
+  TexH t;
+  t.type = TT_NOISE;
+  t.freq = scale;
+  t.grad.assign(grad, grad + 768);
+  t.perm.assign(perm, perm + 768);
+  return push_tex(s, std::move(t), id);
+}
 
 // ---------------------------------------------------------------- materials
 static int push_mat(rtw_scene* s, MatH&& m, uint32_t* id) {
@@ -204,6 +235,12 @@ int rtw_material_metal(rtw_scene* s, float r, float g, float b, float fuzz, uint
 int rtw_material_dielectric(rtw_scene* s, float ir, uint32_t* id) {
   MatH m;
   m.type = MT_DIELECTRIC; m.param = ir;
+  return push_mat(s, std::move(m), id);
+}
+int rtw_material_isotropic(rtw_scene* s, uint32_t tex, uint32_t* id) {
+  if (s && tex >= s->s.tex.size()) return fail(RTW_EINVAL, "texture id out of range");
+  MatH m;
+  m.type = MT_ISOTROPIC; m.tex = tex;
   return push_mat(s, std::move(m), id);
 }
 int rtw_material_diffuse_light(rtw_scene* s, uint32_t tex, uint32_t* id) {
@@ -240,9 +277,22 @@ int rtw_begin_rotate_y(rtw_scene* s, float deg) {
   n.cos_t = cosf(rad);
   return begin(s, std::move(n));
 }
+int rtw_begin_constant_medium(rtw_scene* s, float density, uint32_t tex, uint32_t* material) {
+  if (int e = check_open(s)) return e;
+  if (tex >= s->s.tex.size()) return fail(RTW_EINVAL, "texture id out of range");
+  uint32_t m = 0;
+  if (int e = rtw_material_isotropic(s, tex, &m)) return e;  // volumes.rs:26 Isotropic::new(texture)
+  Node n{NK_MEDIUM, {}};
+  n.f[0] = density;
+  n.mat = m;
+  if (material) *material = m;
+  return begin(s, std::move(n));
+}
 int rtw_end(rtw_scene* s) {
   if (int e = check_open(s)) return e;
   if (s->s.open.size() <= 1) return fail(RTW_ESTATE, "rtw_end without an open group");
+  if (s->s.nodes[s->s.open.back()].kind == NK_MEDIUM && s->s.nodes[s->s.open.back()].ch.size() != 1)
+    return fail(RTW_EINVAL, "ConstantMedium needs exactly one boundary object (volumes.rs:17-21)");
   s->s.open.pop_back();
   return RTW_OK;
 }
@@ -422,13 +472,23 @@ int64_t rtw_scene_info(const rtw_scene* s, int what) {
     case 7: return (int64_t)sc.flat.nodes.size();
     case 8: return (int64_t)sc.flat.stack_need;
     case 9: return (int64_t)sc.flat.features;
+    case 10: return (int64_t)sc.flat.perlins.size();
     case 4: return (int64_t)sc.flat.depth;
     case 5: return (int64_t)sc.flat.always.size();
     case 6: return (int64_t)sc.flat.insts.size();
     default: {
       if (sc.committed) return (int64_t)sc.flat.prims.size();
+      // world leaves in DFS order: a cuboid is six rects, a ConstantMedium one leaf (its boundary
+      // is not part of the world)
       int64_t n = 0;
-      for (const Node& nd : sc.nodes) n += nd.kind == NK_CUBOID ? 6 : (nd.kind >= NK_SPHERE ? 1 : 0);
+      std::vector<uint32_t> todo{0};
+      while (!todo.empty()) {
+        const Node& nd = sc.nodes[todo.back()];
+        todo.pop_back();
+        if (nd.kind == NK_CUBOID) n += 6;
+        else if (nd.kind == NK_MEDIUM || nd.kind >= NK_SPHERE) n += 1;
+        else todo.insert(todo.end(), nd.ch.begin(), nd.ch.end());
+      }
       return n;
     }
   }

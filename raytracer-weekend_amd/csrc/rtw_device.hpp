@@ -23,6 +23,7 @@ enum PrimType : uint32_t {
   PT_RECT_XZ = 3,
   PT_RECT_YZ = 4,
   PT_TRI = 5,
+  PT_MEDIUM = 6,  // ConstantMedium (volumes.rs): boundary sphere / cuboid + density
 };
 
 struct alignas(16) DevPrim {
@@ -31,11 +32,13 @@ struct alignas(16) DevPrim {
   // rect   : q0 = (a0, a1, b0, b1), q1.x = k
   // tri    : q0 = (ax, ay, az, abx), q1 = (aby, abz, acx, acy), q2 = (acz, nx, ny, nz)
   //          ab = b - a, ac = c - a, n = ab x ac (bit-identical to triangular.rs:101-105)
+  // medium : q0 = sphere (cx, cy, cz, r) | cuboid p0 (x, y, z, -), q1 = cuboid p1, q2 = (neg_inv_density,
+  //          boundary kind 0 sphere / 1 cuboid); aux = instance id of the wrappers inside the medium
   float q0[4], q1[4], q2[4];
   uint32_t type_inst;  // bits 0..7 PrimType, bits 8..31 instance id (0 = identity)
   uint32_t key;        // global DFS leaf index: the tie-break (later object wins, mod.rs:61-65)
   uint32_t mat;        // material id
-  uint32_t aux;        // triangle: index into tshade
+  uint32_t aux;        // triangle: index into tshade; medium: inner (boundary) instance id
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
 
@@ -72,18 +75,24 @@ struct alignas(16) DevInst {
   float op[MAX_INST_OPS][4];  // (type, x, y, z) translate  |  (type, sin, cos, 0) rotate_y
 };
 
-enum MatType : uint32_t { MT_LAMBERT = 0, MT_METAL = 1, MT_DIELECTRIC = 2, MT_LIGHT = 3 };
+enum MatType : uint32_t { MT_LAMBERT = 0, MT_METAL = 1, MT_DIELECTRIC = 2, MT_LIGHT = 3, MT_ISOTROPIC = 4 };
 struct alignas(16) DevMat {
   uint32_t type, tex, needs_uv, pad;
   float albedo[3];
   float param;  // metal fuzz | dielectric ir
 };
 
-enum TexType : uint32_t { TT_SOLID = 0, TT_CHECKER = 1, TT_IMAGE = 2, TT_UVDEBUG = 3 };
+enum TexType : uint32_t { TT_SOLID = 0, TT_CHECKER = 1, TT_IMAGE = 2, TT_UVDEBUG = 3, TT_NOISE = 4 };
 struct alignas(16) DevTex {
   uint32_t type, odd, even, pad;
-  float c[3], freq;
-  uint32_t off, w, h, pad2;  // texels[off .. off + 3*w*h)
+  float c[3], freq;          // freq: checker frequency | noise scale
+  uint32_t off, w, h, pad2;  // image: texels[off .. off + 3*w*h) | noise: perlins[off]
+};
+
+// perlin.rs:8-12 Perlin: 256 gradients (xyz, w unused) and the three permutations of 0..255.
+struct alignas(16) DevPerlin {
+  float g[256][4];
+  uint8_t perm[3][256];
 };
 
 // Scene features: the path kernel is instantiated per feature set so a scene only pays (in code
@@ -102,13 +111,17 @@ enum Feature : uint32_t {
   F_METAL = 1u << 10,
   F_DIEL = 1u << 11,
   F_LIGHT = 1u << 12,
+  F_MEDIUM = 1u << 13,  // ConstantMedium primitives
+  F_NOISE = 1u << 14,   // Perlin noise textures
+  F_ISO = 1u << 15,     // Isotropic materials
 };
-constexpr uint32_t F_ALL = (1u << 13) - 1;
+constexpr uint32_t F_ALL = (1u << 16) - 1;
 // Kernel variants (the smallest superset of a scene's features is launched): sphere worlds
-// (jumpy-balls), rect/instance worlds with solid colours (cornell-box), diffuse meshes (cow,
-// monument), and everything.
+// (jumpy-balls), rect/instance worlds with solid colours (cornell-box), the same with media
+// (smokey-cornell-box), diffuse meshes (cow, monument), and everything.
 constexpr uint32_t F_SPHERES = F_SPHERE | F_MSPHERE | F_CHECKER | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
 constexpr uint32_t F_BOXES = F_RECT | F_INST | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
+constexpr uint32_t F_SMOKE = F_BOXES | F_MEDIUM | F_ISO;  // smokey-cornell-box
 constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F_IMAGE | F_LAMBERT | F_LIGHT;
 
 struct DevScene {
@@ -120,6 +133,7 @@ struct DevScene {
   const DevMat* mats;
   const DevTex* texs;
   const uint8_t* texels;
+  const DevPerlin* perlins;
   uint32_t n_nodes, n_prims, n_always, n_insts;
 };
 

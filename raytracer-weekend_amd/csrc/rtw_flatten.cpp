@@ -121,12 +121,14 @@ struct Builder {
     return b;
   }
 
-  void emit(DevPrim p, Box local, const std::vector<uint32_t>& chain) {
+  // box_chain: the wrappers between the box's space and the world (default: the prim's chain)
+  void emit(DevPrim p, Box local, const std::vector<uint32_t>& chain,
+            const std::vector<uint32_t>* box_chain = nullptr) {
     p.type_inst |= instance(chain) << 8;
     p.key = key++;
     Leaf L;
     L.p = p;
-    L.wbox = to_world(local, chain);
+    L.wbox = to_world(local, box_chain ? *box_chain : chain);
     for (int a = 0; a < 3; ++a) L.c[a] = 0.5f * (L.wbox.lo[a] + L.wbox.hi[a]);
     leaves.push_back(L);
   }
@@ -207,6 +209,48 @@ struct Builder {
         rect(1, p0[0], p1[0], p0[2], p1[2], p0[1], n.mat, chain);
         rect(2, p0[1], p1[1], p0[2], p1[2], p1[0], n.mat, chain);
         rect(2, p0[1], p1[1], p0[2], p1[2], p0[0], n.mat, chain);
+        return;
+      }
+      case NK_MEDIUM: {  // volumes.rs:17-83: one leaf; the boundary is geometry of the medium
+        if (n.ch.size() != 1) { err = fail(RTW_EINVAL, "ConstantMedium needs exactly one boundary object"); return; }
+        std::vector<uint32_t> inner;  // wrappers inside the medium, outer -> inner
+        uint32_t b = n.ch[0];
+        for (int guard = 0; guard < 64; ++guard) {
+          const Node& m = s.nodes[b];
+          if ((m.kind == NK_TRANSLATE || m.kind == NK_ROTY || m.kind == NK_LIST || m.kind == NK_BVH) && m.ch.size() == 1) {
+            if (m.kind == NK_TRANSLATE || m.kind == NK_ROTY) inner.push_back(b);
+            b = m.ch[0];
+            continue;
+          }
+          break;
+        }
+        const Node& bd = s.nodes[b];
+        DevPrim p;
+        memset(&p, 0, sizeof p);
+        p.type_inst = PT_MEDIUM;
+        p.q2[0] = -1.0f / n.f[0];  // volumes.rs:25 neg_inv_density
+        p.mat = n.mat;
+        p.aux = instance(inner);
+        Box lb;
+        if (bd.kind == NK_SPHERE) {
+          memcpy(p.q0, bd.f, 4 * sizeof(float));
+          p.q2[1] = 0.0f;
+          float r = fabsf(bd.f[3]);
+          float lo[3] = {bd.f[0] - r, bd.f[1] - r, bd.f[2] - r}, hi[3] = {bd.f[0] + r, bd.f[1] + r, bd.f[2] + r};
+          lb.grow(lo); lb.grow(hi);
+        } else if (bd.kind == NK_CUBOID) {
+          memcpy(p.q0, bd.f, 3 * sizeof(float));
+          memcpy(p.q1, bd.f + 3, 3 * sizeof(float));
+          p.q2[1] = 1.0f;
+          lb.grow(bd.f); lb.grow(bd.f + 3);
+        } else {
+          err = fail(RTW_EINVAL, "ConstantMedium boundary must be a Sphere or a Cuboid (optionally translated / "
+                                 "rotated) in this build");
+          return;
+        }
+        std::vector<uint32_t> full = chain;
+        full.insert(full.end(), inner.begin(), inner.end());
+        emit(p, lb, chain, &full);
         return;
       }
       case NK_TRI: {
@@ -428,7 +472,7 @@ int flatten(Scene& s) {
     memset(&d, 0, sizeof d);
     d.type = m.type; d.tex = m.tex; d.param = m.param;
     memcpy(d.albedo, m.albedo, sizeof d.albedo);
-    d.needs_uv = (m.type == MT_LAMBERT || m.type == MT_LIGHT) ? texture_reads_uv(s, m.tex) : 0;
+    d.needs_uv = (m.type == MT_LAMBERT || m.type == MT_LIGHT || m.type == MT_ISOTROPIC) ? texture_reads_uv(s, m.tex) : 0;
     f.mats.push_back(d);
   }
   for (const TexH& t : s.tex) {
@@ -441,9 +485,20 @@ int flatten(Scene& s) {
       d.w = t.w; d.h = t.h;
       f.texels.insert(f.texels.end(), t.img.begin(), t.img.end());
     }
+    if (t.type == TT_NOISE) {
+      d.off = (uint32_t)f.perlins.size();
+      DevPerlin P;
+      memset(&P, 0, sizeof P);
+      for (int k = 0; k < 256; ++k) {
+        for (int a = 0; a < 3; ++a) P.g[k][a] = t.grad[3 * k + a];
+        for (int a = 0; a < 3; ++a) P.perm[a][k] = (uint8_t)t.perm[256 * a + k];
+      }
+      f.perlins.push_back(P);
+    }
     f.texs.push_back(d);
   }
   if (f.texels.empty()) f.texels.resize(4, 0);
+  if (f.perlins.empty()) f.perlins.resize(1);
   if (f.mats.empty()) f.mats.push_back(DevMat{});
   if (f.texs.empty()) f.texs.push_back(DevTex{});
 
@@ -534,14 +589,16 @@ int flatten(Scene& s) {
   uint32_t F = 0;
   for (const DevPrim& p : f.prims) {
     const uint32_t t = p.type_inst & 0xffu;
-    F |= t == PT_SPHERE ? F_SPHERE : t == PT_MSPHERE ? F_MSPHERE : t == PT_TRI ? F_TRI : F_RECT;
-    if (p.type_inst >> 8) F |= F_INST;
+    F |= t == PT_SPHERE ? F_SPHERE : t == PT_MSPHERE ? F_MSPHERE : t == PT_TRI ? F_TRI : t == PT_MEDIUM ? F_MEDIUM : F_RECT;
+    if ((p.type_inst >> 8) || (t == PT_MEDIUM && p.aux)) F |= F_INST;
     if ((t == PT_SPHERE || t == PT_MSPHERE) && f.mats[p.mat].needs_uv) F |= F_UV;
   }
   for (const DevMat& m : f.mats)
-    F |= m.type == MT_LAMBERT ? F_LAMBERT : m.type == MT_METAL ? F_METAL : m.type == MT_DIELECTRIC ? F_DIEL : F_LIGHT;
+    F |= m.type == MT_LAMBERT ? F_LAMBERT : m.type == MT_METAL ? F_METAL : m.type == MT_DIELECTRIC ? F_DIEL :
+         m.type == MT_ISOTROPIC ? F_ISO : F_LIGHT;
   for (const DevTex& t : f.texs)
-    F |= t.type == TT_CHECKER ? F_CHECKER : t.type == TT_IMAGE ? F_IMAGE : t.type == TT_UVDEBUG ? F_UVDEBUG : 0u;
+    F |= t.type == TT_CHECKER ? F_CHECKER : t.type == TT_IMAGE ? F_IMAGE : t.type == TT_UVDEBUG ? F_UVDEBUG :
+         t.type == TT_NOISE ? F_NOISE : 0u;
   f.features = F;
   // structural self-check: every internal node reached exactly once from the root, every
   // leaf range inside the BVH part of prims[], every BVH prim covered exactly once

@@ -117,6 +117,99 @@ __device__ __forceinline__ V3 rand_in_unit_disk(uint64_t& s) {  // vec3.rs:124-1
   }
 }
 
+// ---- f32 transcendentals, correctly rounded: evaluated in double with polynomials of error
+// < 2^-60 and rounded once (the oracle's §libm restates the same algorithm; tests pin GPU ==
+// oracle == (float)glibc-double).  Only IEEE double + - * / sqrt floor: no FMA contraction
+// (-ffp-contract=off), so the bits are the oracle's.
+__device__ __forceinline__ double ln_core(double m) {  // 2 atanh((m-1)/(m+1)), m in [sqrt(1/2), sqrt(2)]
+  const double s = (m - 1.0) / (m + 1.0), z = s * s;
+  double p = 1.0 / 23.0;
+  p = p * z + 1.0 / 21.0; p = p * z + 1.0 / 19.0; p = p * z + 1.0 / 17.0; p = p * z + 1.0 / 15.0;
+  p = p * z + 1.0 / 13.0; p = p * z + 1.0 / 11.0; p = p * z + 1.0 / 9.0; p = p * z + 1.0 / 7.0;
+  p = p * z + 1.0 / 5.0; p = p * z + 1.0 / 3.0; p = p * z + 1.0;
+  return 2.0 * s * p;
+}
+__device__ __forceinline__ float dev_log10f(float x) {  // f32::log10
+  if (x != x) return x;
+  if (x == 0.0f) return -INFINITY;
+  if (x < 0.0f) return NAN;
+  if (isinf(x)) return x;
+  const uint64_t u = (uint64_t)__double_as_longlong((double)x);
+  int e = (int)((u >> 52) & 0x7ff) - 1023;
+  double m = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+  if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+  const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+  const double INV_LN10 = 0.43429448190325182765;
+  const double lnx = ((double)e * LN2_HI + ln_core(m)) + (double)e * LN2_LO;
+  return (float)(lnx * INV_LN10);
+}
+__device__ __forceinline__ double sin_core(double r) {
+  const double z = r * r;
+  double p = -1.0 / 1307674368000.0;
+  p = p * z + 1.0 / 6227020800.0; p = p * z - 1.0 / 39916800.0; p = p * z + 1.0 / 362880.0;
+  p = p * z - 1.0 / 5040.0; p = p * z + 1.0 / 120.0; p = p * z - 1.0 / 6.0;
+  return r + r * z * p;
+}
+__device__ __forceinline__ double cos_core(double r) {
+  const double z = r * r;
+  double p = 1.0 / 20922789888000.0;
+  p = p * z - 1.0 / 87178291200.0; p = p * z + 1.0 / 479001600.0; p = p * z - 1.0 / 3628800.0;
+  p = p * z + 1.0 / 40320.0; p = p * z - 1.0 / 720.0; p = p * z + 1.0 / 24.0; p = p * z - 0.5;
+  return 1.0 + z * p;
+}
+__device__ __forceinline__ float dev_sinf(float x) {  // f32::sin
+  if (x != x || x == 0.0f) return x;  // keeps the sign of zero
+  if (isinf(x)) return NAN;
+  const double d = x;
+  const double TWO_OVER_PI = 6.36619772367581382433e-01;
+  const double P1 = 1.57079632673412561417e+00, P2 = 6.07710050650619224932e-11, P3 = 2.02226624879595063154e-21;
+  const double k = floor(d * TWO_OVER_PI + 0.5);
+  const double r = ((d - k * P1) - k * P2) - k * P3;
+  const double q = k - 4.0 * floor(k * 0.25);
+  const double v = q == 0.0 ? sin_core(r) : (q == 1.0 ? cos_core(r) : (q == 2.0 ? -sin_core(r) : -cos_core(r)));
+  return (float)v;
+}
+__device__ __forceinline__ double atan_core(double t) {  // |t| <= tan(pi/16)
+  const double z = t * t;
+  double p = -1.0 / 29.0;
+  p = p * z + 1.0 / 27.0; p = p * z - 1.0 / 25.0; p = p * z + 1.0 / 23.0; p = p * z - 1.0 / 21.0;
+  p = p * z + 1.0 / 19.0; p = p * z - 1.0 / 17.0; p = p * z + 1.0 / 15.0; p = p * z - 1.0 / 13.0;
+  p = p * z + 1.0 / 11.0; p = p * z - 1.0 / 9.0; p = p * z + 1.0 / 7.0; p = p * z - 1.0 / 5.0;
+  p = p * z + 1.0 / 3.0;
+  return t - t * z * p;
+}
+__device__ __forceinline__ double atan01(double a) {  // 0 <= a <= 1
+  const double T1 = 0.19891236737965800691, T3 = 0.66817863791929891999, C1 = 0.41421356237309504880;
+  const double PI_8 = 0.39269908169872415481, PI_4 = 0.78539816339744830962;
+  if (a <= T1) return atan_core(a);
+  if (a <= T3) return PI_8 + atan_core((a - C1) / (1.0 + a * C1));
+  return PI_4 + atan_core((a - 1.0) / (1.0 + a));
+}
+__device__ __forceinline__ double atan2_pos(double y, double x) {  // y > 0 finite, x finite non-zero
+  const double PI = 3.14159265358979323846, PI_2 = 1.57079632679489661923;
+  const double ax = fabs(x);
+  const double r = y <= ax ? atan01(y / ax) : PI_2 - atan01(ax / y);
+  return x < 0.0 ? PI - r : r;
+}
+__device__ __forceinline__ float dev_atan2f(float y, float x) {  // f32::atan2, C99 Annex F special cases
+  const double PI = 3.14159265358979323846, PI_2 = 1.57079632679489661923, PI_4 = 0.78539816339744830962;
+  if (x != x || y != y) return x + y;
+  const bool sx = signbit(x), sy = signbit(y);
+  double r;
+  if (y == 0.0f) r = sx ? PI : 0.0;
+  else if (isinf(x)) r = isinf(y) ? (sx ? 3.0 * PI_4 : PI_4) : (sx ? PI : 0.0);
+  else if (x == 0.0f || isinf(y)) r = PI_2;
+  else r = atan2_pos(fabs((double)y), (double)x);
+  return (float)(sy ? -r : r);
+}
+__device__ __forceinline__ float dev_acosf(float x) {  // f32::acos = atan2(sqrt((1-x)(1+x)), x)
+  if (x != x) return x;
+  if (!(fabsf(x) <= 1.0f)) return NAN;
+  const double d = x, s = sqrt((1.0 - d) * (1.0 + d));
+  if (s == 0.0) return d > 0.0 ? 0.0f : (float)3.14159265358979323846;
+  return (float)atan2_pos(s, d);
+}
+
 struct Ray { V3 o, d; float time; };
 
 // ---- wrapper chains (transformations.rs:23-38, :115-135): world ray -> object ray
@@ -188,6 +281,78 @@ __device__ __forceinline__ float cand_tri(const Ray& r, const float* q) {
 
 struct Best { float t; uint32_t key; int32_t prim; };
 
+// ConstantMedium::hit (volumes.rs:37-78) in the order-independent form the oracle defines (K_MEDIUM):
+// boundary entry / exit by the reference's own hit routines with t in (-inf, inf) and
+// (rec1 + 0.0001, inf), distance test against the unclipped exit, and the draw from a sub-stream
+// keyed by (segment state, leaf key).  -1 = no hit.
+template <uint32_t FEAT>
+__device__ __forceinline__ float cand_medium(const DevScene& S, const Ray& lr, const float4* P, uint32_t key,
+                                          uint32_t inner, uint64_t seg) {
+  const float4 q0v = P[0], q1v = P[1], q2v = P[2];
+  const Ray br = ((FEAT & F_INST) && inner) ? to_local(S.insts + inner, lr) : lr;
+  float r1, r2;
+  if (q2v.y == 0.0f) {  // Sphere boundary: spherical.rs:18-60 twice
+    const V3 oc = sub(br.o, mk(q0v.x, q0v.y, q0v.z));
+    const float a = len2(br.d), hb = dot(oc, br.d), cc = len2(oc) - q0v.w * q0v.w;
+    const float disc = hb * hb - a * cc;
+    if (disc < 0.0f) return -1.0f;
+    const float sq = sqrtf(disc);
+    const float root1 = (-hb - sq) / a, root2 = (-hb + sq) / a;
+    float rt = root1;
+    if (rt < -INFINITY || INFINITY < rt) {
+      rt = root2;
+      if (rt < -INFINITY || INFINITY < rt) return -1.0f;
+    }
+    r1 = rt;
+    const float lo = r1 + 0.0001f;
+    rt = root1;
+    if (rt < lo || INFINITY < rt) {
+      rt = root2;
+      if (rt < lo || INFINITY < rt) return -1.0f;
+    }
+    r2 = rt;
+  } else {  // Cuboid boundary: its six rects (rectangular.rs:177-240) as a closest-hit list, twice
+    const float p0[3] = {q0v.x, q0v.y, q0v.z}, p1[3] = {q1v.x, q1v.y, q1v.z};
+    const float o[3] = {br.o.x, br.o.y, br.o.z}, d[3] = {br.d.x, br.d.y, br.d.z};
+    float ts[6];
+    bool inb[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int axis = k >> 1;  // XY, XY, XZ, XZ, YZ, YZ; k on z / y / x, far side first
+      const int kx = axis == 0 ? 2 : (axis == 1 ? 1 : 0), ax = axis == 2 ? 1 : 0, bx = axis == 0 ? 1 : 2;
+      const float kk = (k & 1) ? p0[kx] : p1[kx];
+      const float t = (kk - o[kx]) / d[kx];
+      const float x = o[ax] + t * d[ax], y = o[bx] + t * d[bx];
+      ts[k] = t;
+      inb[k] = !(x < p0[ax] || x > p1[ax] || y < p0[bx] || y > p1[bx]);
+    }
+    float closest = INFINITY;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (inb[k] && !(ts[k] < -INFINITY || ts[k] > closest)) { closest = ts[k]; any = true; }
+    if (!any) return -1.0f;
+    r1 = closest;
+    const float lo = r1 + 0.0001f;
+    closest = INFINITY;
+    any = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (inb[k] && !(ts[k] < lo || ts[k] > closest)) { closest = ts[k]; any = true; }
+    if (!any) return -1.0f;
+    r2 = closest;
+  }
+  float t1 = fmaxf(r1, TMIN);
+  if (t1 >= r2) return -1.0f;
+  t1 = fmaxf(t1, 0.0f);
+  const float len = sqrtf(len2(lr.d));
+  const float dist = (r2 - t1) * len;
+  uint64_t g = splitmix64(seg ^ splitmix64((uint64_t)key));
+  const float hd = q2v.x * dev_log10f(gen_f32(g));
+  if (hd > dist) return -1.0f;
+  return t1 + hd / len;
+}
+
 // COUNT build only: wave-level SIMD utilisation.  Adds 1 to cnt[wave_slot] for the first
 // active lane (one per wave execution) and the wave's active-lane count to cnt[lane_slot].
 __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane_slot) {
@@ -200,7 +365,7 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
 
 template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
-                                          uint32_t* cnt) {
+                                          uint32_t* cnt, uint64_t seg) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
   const float4 q0v = P[0];
@@ -221,13 +386,15 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     const float4 q1v = P[1], q2v = P[2];
     const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
     t = cand_tri(lr, q);
+  } else if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {
+    t = cand_medium<FEAT>(S, lr, P, meta.y, meta.w, seg);
   } else if (FEAT & F_RECT) {
     const float k = P[1].x;
     if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
     else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
     else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
   }
-  if (COUNT) { cnt[1]++; cnt[2 + type]++; simd_tick(cnt, 10, 11); }
+  if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }  // media: total only
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
   if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && meta.y > b.key))) {
     b.t = t;
@@ -260,9 +427,10 @@ struct TraceState {
 };
 
 template <bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt) {
+__device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
+                                            uint64_t seg) {
   ts.b = Best{INFINITY, 0u, -1};
-  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt);
+  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt, seg);
   ts.node = S.n_nodes ? 0 : -1;
   ts.pend = 0;
   ts.sp = 0;
@@ -275,7 +443,7 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // every lane of the wave holds a leaf or has run dry; phase 2 tests all parked leaves together.
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
-                          uint32_t spill_lanes, uint32_t* cnt, uint32_t quota) {
+                          uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint64_t seg) {
   auto safe_inv = [](float d) {
     float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
     return __builtin_amdgcn_rcpf(dd);
@@ -369,7 +537,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     if (ts.pend != 0) {  // phase 2
       const uint32_t v = ~(uint32_t)ts.pend;
       const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
-      for (int32_t k = 0; k < n; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt);
+      for (int32_t k = 0; k < n; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg);
       ts.pend = 0;
     }
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
@@ -385,8 +553,8 @@ __device__ __forceinline__ void face(Rec& h, V3 dir, V3 outward) {
 }
 __device__ __forceinline__ void sphere_uv(V3 p, float& u, float& v) {  // spherical.rs:62-77
   const float PI = 3.14159265358979323846f;
-  float theta = acosf(-p.y);
-  float phi = atan2f(-p.z, p.x) + PI;
+  float theta = dev_acosf(-p.y);
+  float phi = dev_atan2f(-p.z, p.x) + PI;
   u = phi / (2.0f * PI);
   v = theta / PI;
 }
@@ -418,6 +586,8 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
     outward = add(add(scale(ld3(sh.n), w), scale(ld3(sh.n + 3), s.u)), scale(ld3(sh.n + 6), s.v));
     h.u = (w * sh.uv[0] + s.u * sh.uv[2]) + s.v * sh.uv[4];
     h.v = (w * sh.uv[1] + s.u * sh.uv[3]) + s.v * sh.uv[5];
+  } else if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {  // volumes.rs:62-77: no face-normal logic
+    outward = mk(1.0f, 0.0f, 0.0f);
   } else {
     const int axis = (int)type - PT_RECT_XY;
     const float x = axis == 2 ? h.p.y : h.p.x;
@@ -426,7 +596,12 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
     h.v = (y - P.q0[2]) / (P.q0[3] - P.q0[2]);
     outward = axis == 0 ? mk(0.f, 0.f, 1.f) : (axis == 1 ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f));
   }
-  face(h, lr.d, outward);
+  if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {
+    h.n = outward;
+    h.front = true;
+  } else {
+    face(h, lr.d, outward);
+  }
   if ((FEAT & F_INST) && inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
     for (int k = (int)I->nops - 1; k >= 0; --k) {
       V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
@@ -468,7 +643,48 @@ __device__ __forceinline__ bool checker_odd(float fx, float fy, float fz) {
   return sinf(fx) * sinf(fy) * sinf(fz) < 0.0f;
 }
 
-// ---- textures (texture.rs:56-81, :97-104; image_texture.rs:34-52)
+// ---- Perlin noise (perlin.rs:50-122), same operation order as the oracle's perlin_noise
+__device__ __forceinline__ int64_t f32_as_i64(float x) {  // Rust `as i64`: saturating, NaN -> 0
+  if (x != x) return 0;
+  if (x >= 9223372036854775807.0f) return INT64_MAX;
+  if (x <= -9223372036854775808.0f) return INT64_MIN;
+  return (int64_t)x;
+}
+__device__ __forceinline__ float perlin_noise(const DevPerlin& P, V3 p) {
+  const V3 fl = mk(floorf(p.x), floorf(p.y), floorf(p.z));
+  const uint32_t bx = (uint32_t)f32_as_i64(fl.x), by = (uint32_t)f32_as_i64(fl.y), bz = (uint32_t)f32_as_i64(fl.z);
+  const V3 w = sub(p, fl);
+  const V3 f = mul(mul(w, w), sub(mk(3.0f, 3.0f, 3.0f), scale(w, 2.0f)));  // filter_hermit
+  float accum = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t hsh = (uint32_t)P.perm[0][(bx + i) & 255u] ^ (uint32_t)P.perm[1][(by + j) & 255u] ^
+                             (uint32_t)P.perm[2][(bz + k) & 255u];
+        const float4 g = *reinterpret_cast<const float4*>(P.g[hsh]);
+        const V3 c = mk((float)i, (float)j, (float)k);
+        const V3 wv = sub(f, c);
+        const V3 bl = add(mul(c, f), mul(sub(mk(1.f, 1.f, 1.f), c), sub(mk(1.f, 1.f, 1.f), f)));
+        const float bf = bl.x * bl.y * bl.z;
+        accum += bf * dot(mk(g.x, g.y, g.z), wv);
+      }
+  return accum;
+}
+__device__ __forceinline__ float perlin_turbulence(const DevPerlin& P, V3 p, int depth) {  // perlin.rs:78-91
+  float accum = 0.0f, weight = 1.0f;
+#pragma unroll 1
+  for (int d = 0; d < depth; ++d) {
+    accum += weight * perlin_noise(P, p);
+    weight *= 0.5f;
+    p = scale(p, 2.0f);
+  }
+  return fabsf(accum);
+}
+
+// ---- textures (texture.rs:56-81, :89-104; image_texture.rs:34-52)
 template <uint32_t FEAT>
 __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) {
   for (int guard = 0; guard < 64; ++guard) {
@@ -491,7 +707,12 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
       const float sc = 1.0f / 255.0f;
       return mk((float)px[0] * sc, (float)px[1] * sc, (float)px[2] * sc);
     }
-    if (FEAT & F_UVDEBUG) return mk(u, v, 0.0f);  // UVDebug
+    if ((FEAT & F_NOISE) && t.type == TT_NOISE) {  // texture.rs:89-95
+      const float tb = perlin_turbulence(S.perlins[t.off], p, 7);
+      const float sv = 0.5f * (1.0f + dev_sinf(t.freq * p.z + 10.0f * tb));
+      return mk(sv, sv, sv);
+    }
+    if ((FEAT & F_UVDEBUG) && t.type == TT_UVDEBUG) return mk(u, v, 0.0f);  // UVDebug
     break;
   }
   return mk(0.f, 0.f, 0.f);
@@ -623,11 +844,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
     if (!ts.on) {
       ++nrays;
-      trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt);
+      trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     }
     {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota);
+      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng);
     }
     phase(1);
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
@@ -661,6 +882,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
         } else {
           done = true;  // absorbed: emitted() is black
         }
+      } else if ((FEAT & F_ISO) && m.type == MT_ISOTROPIC) {  // material.rs:155-165, never absorbs
+        st.T = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
+        st.ray.o = h.p;
+        st.ray.d = rand_in_unit_sphere(st.rng);
       } else if (FEAT & F_DIEL) {  // Dielectric, material.rs:116-142
         const float ratio = h.front ? 1.0f / m.param : m.param;
         const V3 ud = unit(st.ray.d);
@@ -731,6 +956,14 @@ __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, co
   for (int c = 0; c < 3; ++c) img[((size_t)row * w + i) * 3 + c] = packed[(size_t)g * 3 + c];
 }
 
+// Diagnostics (rtw_diag_libm): the render path's f32 transcendentals over arrays.
+__global__ void libm_kernel(int fn, uint32_t n, const float* a, const float* b, float* out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const float x = a[g];
+  out[g] = fn == 0 ? dev_log10f(x) : (fn == 1 ? dev_sinf(x) : (fn == 2 ? dev_acosf(x) : dev_atan2f(x, b[g])));
+}
+
 }  // namespace dev
 
 // ---------------------------------------------------------------- host side
@@ -760,7 +993,7 @@ int upload(Scene& s, int device) {
   std::vector<uint8_t> blob;
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
-  size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels);
+  size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
   blob.resize((blob.size() + 255) & ~(size_t)255);
   int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
   int prev = 0;
@@ -782,6 +1015,7 @@ int upload(Scene& s, int device) {
     c.scene.mats = (const DevMat*)(base + o_mat);
     c.scene.texs = (const DevTex*)(base + o_tex);
     c.scene.texels = (const uint8_t*)(base + o_texel);
+    c.scene.perlins = (const DevPerlin*)(base + o_perlin);
     c.scene.n_nodes = (uint32_t)f.nodes4.size();
     c.scene.n_prims = (uint32_t)f.prims.size();
     c.scene.n_always = (uint32_t)f.always.size();
@@ -848,6 +1082,7 @@ static path_fn pick_kernel(uint32_t feat, uint32_t need) {
       if (env_int("RTW_GENERIC", 0)) return pick5<C, F_ALL>(need);  // parity of the generic kernel
       if (sph) return pick5<C, F_SPHERES>(need);
       if ((feat & ~F_BOXES) == 0) return pick5<C, F_BOXES>(need);
+      if ((feat & ~F_SMOKE) == 0) return pick5<C, F_SMOKE>(need);
       if ((feat & ~F_MESHES) == 0) return pick5<C, F_MESHES>(need);
       return pick5<C, F_ALL>(need);
   }
@@ -1073,6 +1308,31 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
   }
   c->kev_count = 0;
   hipSetDevice(prev);
+  return rc;
+}
+
+int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out) {
+  if (fn < 0 || fn > 3 || (n && (!a || !out || (fn == 3 && !b)))) return fail(RTW_EINVAL, "bad arguments");
+  if (!n) return RTW_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
+  float *da = nullptr, *db = nullptr, *dout = nullptr;
+  const size_t bytes = (size_t)n * sizeof(float);
+  int rc = RTW_OK;
+  if (hipMalloc((void**)&da, bytes) != hipSuccess || hipMalloc((void**)&dout, bytes) != hipSuccess ||
+      (fn == 3 && hipMalloc((void**)&db, bytes) != hipSuccess)) {
+    rc = fail(RTW_ENOMEM, "hipMalloc(diag)");
+  } else if (hipMemcpy(da, a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+             (db && hipMemcpy(db, b, bytes, hipMemcpyHostToDevice) != hipSuccess)) {
+    rc = fail(RTW_ENODEV, "hipMemcpy(diag)");
+  } else {
+    hipLaunchKernelGGL(dev::libm_kernel, dim3((n + 255) / 256), dim3(256), 0, nullptr, fn, n, da, db, dout);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(RTW_ENODEV, "libm_kernel");
+  }
+  if (da) hipFree(da);
+  if (db) hipFree(db);
+  if (dout) hipFree(dout);
   return rc;
 }
 

@@ -25,6 +25,7 @@ enum NodeKind : uint32_t {
   NK_RECT,       // XY/XZ/YZRectangle                   rectangular.rs:16-166
   NK_CUBOID,     // Cuboid (six rects)                  rectangular.rs:170-245
   NK_TRI,        // Triangle                            triangular.rs:33-149
+  NK_MEDIUM,     // ConstantMedium(boundary, density)   volumes.rs:17-83 (f[0] density, mat = Isotropic)
 };
 
 struct Node {
@@ -41,6 +42,8 @@ struct TexH {
   float freq = 0.f;
   uint32_t w = 0, h = 0;
   std::vector<uint8_t> img;
+  std::vector<float> grad;     // noise: 256 x 3 gradients (perlin.rs:16-19)
+  std::vector<uint32_t> perm;  // noise: 3 x 256 permutations (perlin.rs:21-23)
 };
 
 struct MatH {
@@ -61,6 +64,7 @@ struct Flat {
   std::vector<DevMat> mats;
   std::vector<DevTex> texs;
   std::vector<uint8_t> texels;
+  std::vector<DevPerlin> perlins;
   uint32_t depth = 0;
   uint32_t features = 0;  // Feature bits actually used
   float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover

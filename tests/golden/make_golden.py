@@ -3,8 +3,11 @@
 Written separately from oracle/rtw_oracle.c (not a translation of it) straight from the
 reference lines cited below, to pin the C oracle: tests/test_golden.py checks the oracle
 bit-for-bit against the vectors this script writes to tests/golden/golden.npz.
-Transcendentals call the C library's tanf/sinf/cosf/acosf/atan2f through ctypes — the same
-libm functions Rust's f32 methods call in the reference build.
+tanf/sinf/cosf (camera and YRotation set-up, host side) call the C library through ctypes —
+the libm functions Rust's f32 methods call in the reference build.  acosf/atan2f (sphere uv, on
+the render path) are the correctly rounded values, (float) of the f64 result: glibc's f32
+versions are only faithfully rounded and other platforms differ, so this build defines the
+render path's transcendentals as correctly rounded (rtw_oracle.c §libm).
 
     python tests/golden/make_golden.py        # rewrites tests/golden/golden.npz
 """
@@ -29,8 +32,8 @@ _libm.atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
 def tanf(x): return F(_libm.tanf(float(x)))
 def sinf(x): return F(_libm.sinf(float(x)))
 def cosf(x): return F(_libm.cosf(float(x)))
-def acosf(x): return F(_libm.acosf(float(x)))
-def atan2f(y, x): return F(_libm.atan2f(float(y), float(x)))
+def acosf(x): return F(math.acos(float(x)))                 # correctly rounded (see docstring)
+def atan2f(y, x): return F(math.atan2(float(y), float(x)))
 
 
 # ------------------------------------------------------------------ bit sources (this build's RNG)
@@ -388,6 +391,90 @@ def render_jumpy(w, h, spp, scene_seed, seed, aspect):
     return img, rays, cam
 
 
+# ------------------------------------------------------------------ Perlin (perlin.rs), Noise (texture.rs:89-95)
+def log10f(x): return F(-np.inf) if x == 0 else F(math.log10(float(x)))   # correctly rounded
+def sinf_cr(x): return F(math.sin(float(x)))
+
+
+def perlin_noise(grad, perm, p):  # perlin.rs:50-76, interp :93-117 (filtered point for both uses)
+    fl = np.floor(p).astype(np.float32)
+    base = [int(x) for x in fl]
+    w = (p - fl).astype(np.float32)
+    f = ((w * w).astype(np.float32) * (F(3.0) - F(2.0) * w).astype(np.float32)).astype(np.float32)
+    acc = F(0.0)
+    one = v(1, 1, 1)
+    for i in range(2):
+        for j in range(2):
+            for k in range(2):
+                hsh = perm[0][(base[0] + i) & 255] ^ perm[1][(base[1] + j) & 255] ^ perm[2][(base[2] + k) & 255]
+                c = v(i, j, k)
+                wv = (f - c).astype(np.float32)
+                bl = ((c * f).astype(np.float32) + ((one - c) * (one - f)).astype(np.float32)).astype(np.float32)
+                bf = F(F(bl[0] * bl[1]) * bl[2])
+                acc = F(acc + F(bf * dot(grad[hsh], wv)))
+    return acc
+
+
+def turbulence(grad, perm, p, depth=7):  # perlin.rs:78-91
+    acc, weight, tp = F(0.0), F(1.0), p.astype(np.float32)
+    for _ in range(depth):
+        acc = F(acc + F(weight * perlin_noise(grad, perm, tp)))
+        weight = F(weight * F(0.5))
+        tp = (tp * F(2.0)).astype(np.float32)
+    return F(abs(acc))
+
+
+def perlin_new(d):  # perlin.rs:14-48 with the scene stream; usize gen_range(0..i) as a widening multiply
+    grad = np.array([unit(v(d.gen_range(-1, 1), d.gen_range(-1, 1), d.gen_range(-1, 1))) for _ in range(256)],
+                    np.float32)
+    perms = []
+    for _ in range(3):
+        p = list(range(256))
+        for i in range(255, 0, -1):
+            t = (d.u32() * i) >> 32
+            p[i], p[t] = p[t], p[i]
+        perms.append(p)
+    return grad, np.array(perms, np.uint32)
+
+
+# ------------------------------------------------------------------ ConstantMedium (volumes.rs:37-78)
+def medium_hit(kind, par, o, d, tmin, tmax, density, seg, key):
+    """The build's order-independent form: rec2 unclipped, draw from the (segment, key) sub-stream."""
+    neg_inv = F(F(-1.0) / F(density))
+    def boundary(lo):
+        if kind == 0:
+            h = hit_sphere(o, d, F(lo), F(np.inf), par[:3], par[3])
+            return None if h is None else h[0]
+        p0, p1 = par[:3], par[3:6]
+        sides = [(0, p0[0], p1[0], p0[1], p1[1], p1[2]), (0, p0[0], p1[0], p0[1], p1[1], p0[2]),
+                 (1, p0[0], p1[0], p0[2], p1[2], p1[1]), (1, p0[0], p1[0], p0[2], p1[2], p0[1]),
+                 (2, p0[1], p1[1], p0[2], p1[2], p1[0]), (2, p0[1], p1[1], p0[2], p1[2], p0[0])]
+        closest, found = F(np.inf), None
+        for sd in sides:  # Cuboid::hit = the six rects as a closest-hit list (rectangular.rs:238-240)
+            h = hit_rect(o, d, F(lo), closest, *sd)
+            if h is not None:
+                closest, found = h[0], h[0]
+        return found
+    r1 = boundary(-np.inf)
+    if r1 is None:
+        return None
+    r2 = boundary(F(r1 + F(0.0001)))
+    if r2 is None:
+        return None
+    t1 = F(max(r1, F(tmin)))
+    if t1 >= r2:
+        return None
+    t1 = F(max(t1, F(0.0)))
+    ln = F(np.sqrt(len2(d)))
+    dist = F(F(r2 - t1) * ln)
+    u = Pcg32(splitmix64(seg ^ splitmix64(key))).next_u32()
+    hd = F(neg_inv * log10f(F(u >> 8) * F(1.0 / 16777216.0)))
+    if hd > dist:
+        return None
+    t = F(t1 + F(hd / ln))
+    return None if t > tmax else t
+
+
 def main():
     rng = np.random.default_rng(20240807)
     g = {}
@@ -512,6 +599,37 @@ def main():
     g["jumpy_rays"] = np.array([nrays])
     sph, mats = jumpy_balls(5)
     g["jumpy_spheres"] = np.array([[*s[0], s[1], *s[2], s[3], s[4], s[5], s[6]] for s in sph], np.float32)
+    # Perlin noise / turbulence over random tables (perlin.rs:50-122) and Perlin::new (perlin.rs:14-48)
+    pg = np.array([unit(x) for x in rng.normal(0, 1, (256, 3)).astype(np.float32)], np.float32)
+    pp = np.stack([rng.permutation(256) for _ in range(3)]).astype(np.uint32)
+    pts = rng.uniform(-20, 20, (96, 3)).astype(np.float32)
+    pts[:8] = np.floor(pts[:8])  # lattice points
+    pts[8:16] *= np.float32(40.0)  # beyond one period of the 256-wide lattice
+    g["perlin_grad"], g["perlin_perm"], g["perlin_pts"] = pg, pp, pts
+    g["perlin_noise"] = np.array([perlin_noise(pg, pp, p) for p in pts], np.float32)
+    g["perlin_turb"] = np.array([turbulence(pg, pp, p, 7) for p in pts], np.float32)
+    g["noise_value"] = np.array([F(F(0.5) * F(F(1.0) + sinf_cr(F(F(F(4.0) * p[2]) + F(F(10.0) * t)))))
+                                 for p, t in zip(pts, g["perlin_turb"])], np.float32)
+    ng, npm = perlin_new(Draws(scene_rng(7)))
+    g["perlin_new_grad"], g["perlin_new_perm"] = ng, npm
+    # ConstantMedium hits (sphere and cuboid boundaries)
+    med_in, med_out = [], []
+    for q in range(160):
+        kind = q % 2
+        par = (np.array([0.2, -0.1, 0.3, 1.3, 0, 0], np.float32) if kind == 0
+               else np.array([-1.0, -0.7, -1.2, 0.9, 1.1, 0.8], np.float32))
+        dens = [0.05, 0.5, 5.0, 50.0][q % 4]
+        o = rng.uniform(-3, 3, 3).astype(np.float32)
+        if q % 5 == 0:
+            o = rng.uniform(-0.5, 0.5, 3).astype(np.float32)  # starting inside
+        d = (rng.uniform(-0.5, 0.5, 3) - o).astype(np.float32)
+        seg = int(rng.integers(0, 2 ** 63))
+        key = int(rng.integers(0, 4000))
+        t = medium_hit(kind, par, o, d, 0.001, np.inf, dens, seg, key)
+        med_in.append([kind, dens, *par, *o, *d, 0.5, seg & 0xFFFFFFFF, seg >> 32, key])
+        med_out.append([0.0, 0.0] if t is None else [1.0, t])
+    g["medium_in"] = np.array(med_in, np.float64)
+    g["medium_out"] = np.array(med_out, np.float32)
     out = Path(__file__).resolve().parent / "golden.npz"
     np.savez_compressed(out, **g)
     print("wrote", out, "keys", len(g), "jumpy rays", nrays)

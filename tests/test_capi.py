@@ -7,6 +7,8 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+REF_MODELS = Path("/root/reference/models")
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -108,8 +110,18 @@ def test_flatten_self_check(rtw, name):
 def test_presets_unknown_scene(rtw):
     s = rtw.Scene()
     with pytest.raises(rtw.RtwError) as e:
-        s.preset("book2-final-scene", 1.0)
-    assert "out-of-scope" in str(e.value)
+        s.preset("no-such-scene", 1.0)
+    assert "unknown" in str(e.value)
+
+
+@pytest.mark.skipif(not (REF_MODELS / "Normals_Try3.obj").exists(), reason="reference models not mounted")
+def test_suspension_obj_fails_like_the_reference(rtw):
+    """scenes.rs:773-814 loads Normals_Try3.obj, whose `usemtl` has no `mtllib`: the reference
+    panics at triangular.rs:176 (unwrap); the preset returns RTW_EIO."""
+    s = rtw.Scene()
+    with pytest.raises(rtw.RtwError) as e:
+        s.preset("wavefront-suspension-obj", 16 / 9, models_dir=REF_MODELS)
+    assert e.value.code == rtw.RTW_EIO and "usemtl without mtllib" in str(e.value)
 
 
 def test_image_height_rule(rtw):

@@ -18,6 +18,13 @@ SCENES = [
     ("textured-monument", 16 / 9, 48, 27, 3),
     ("two-spheres", 16 / 9, 48, 27, 4),
     ("simple-triangle", 16 / 9, 48, 27, 4),
+    # Perlin noise, image-textured spheres (uv), media, the book-2 scenes
+    ("two-perlin-spheres", 16 / 9, 48, 27, 3),
+    ("earth", 16 / 9, 48, 27, 3),
+    ("simple-light", 16 / 9, 48, 27, 4),
+    ("smokey-cornell-box", 1.0, 32, 32, 6),
+    ("book2-final-scene", 1.0, 32, 32, 3),
+    ("animated-book2-final-scene", 1.0, 24, 24, 2),
 ]
 
 
@@ -126,3 +133,32 @@ def test_generic_kernel_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp
     g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
     assert st["rays"] == rays
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def test_device_libm_equals_oracle(gpu, orc):
+    """The kernel's f32 transcendentals (double-evaluated, correctly rounded) are the oracle's,
+    bit for bit: every rand Standard<f32> value for log10 (the medium draw), dense strides of the
+    float line for acos (sphere uv) and sin (Noise), random pairs and IEEE specials for atan2."""
+    rtw = gpu
+    u = (np.arange(1, 1 << 24, dtype=np.float64) * 2.0 ** -24).astype(np.float32)
+    u = np.concatenate([u, np.array([0.0, -0.0, 1.0, np.inf, -1.0, np.nan, 1e-45, 3e38], np.float32)])
+    b = np.arange(0, 0x3F800001, 37, dtype=np.uint32)
+    ac = np.concatenate([b, b | np.uint32(0x80000000)]).view(np.float32)
+    b = np.arange(0, 0x47000000, 97, dtype=np.uint32)
+    sn = np.concatenate([b, b | np.uint32(0x80000000), np.array([0x7F800000, 0xFF800000, 0x7FC00000,
+                                                                  0x4F000000, 0x5F000000], np.uint32)]).view(np.float32)
+    rng = np.random.default_rng(11)
+    e = rng.integers(90, 160, (2, 1 << 20))
+    m = rng.integers(0, 1 << 23, (2, 1 << 20))
+    sg = rng.integers(0, 2, (2, 1 << 20))
+    ab = ((sg << 31) | (e << 23) | m).astype(np.uint32).view(np.float32)
+    sp = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 3e38], np.float32)
+    y, x = np.meshgrid(sp, sp)
+    ay = np.concatenate([ab[0], y.ravel()])
+    ax = np.concatenate([ab[1], x.ravel()])
+    for fn, a, bb in ((0, u, None), (1, sn, None), (2, ac, None), (3, ay, ax)):
+        dev = rtw.diag_libm(fn, a, bb)
+        ref = orc.libm(fn, a, bb)
+        same = (dev.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(dev) & np.isnan(ref))
+        bad = np.nonzero(~same)[0]
+        assert bad.size == 0, (fn, bad.size, a[bad[:4]], dev[bad[:4]], ref[bad[:4]])
