@@ -174,6 +174,37 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float background[3], u
                uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, float* out_rgb_sum,
                rtw_stats* stats);
 
+/* lib.rs:120-126 Pixel: row j (0 = bottom), column i, un-normalised Σ over spp. */
+typedef struct {
+  uint32_t row, column;
+  float color[3];
+} rtw_pixel;
+/* Receives the next n pixels of the stream; a non-zero return stops the render (returned as is). */
+typedef int (*rtw_pixel_sink)(const rtw_pixel* pixels, uint32_t n, void* user);
+
+/* Raytracer::render() as a progressive stream (lib.rs:50-76 RenderIterator): the frame is rendered
+ * in bands of `band_rows` output rows (rounded up to whole 8-row tile rows; 0 = 64) and each band's
+ * pixels are handed to `sink` in the reference's emission order (row j = h-1 .. 0, column 0 .. w-1)
+ * as soon as the band is done.  Same pixels as rtw_render. */
+int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float background[3], uint32_t w,
+                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, uint32_t band_rows,
+                      rtw_pixel_sink sink, void* user, rtw_stats* stats);
+
+/* lib.rs:128-138 ProgressMessage on the wire (discovery_app/src/bin/raytracer.rs:62-113 ->
+ * discovery_host_receiver/src/main.rs:22-110): postcard 0.7.3 (Cargo.lock:2533-2541; enum tag and
+ * u32 as varints, f32 little-endian, Color as its 3-float array) framed by COBS (postcard-cobs
+ * 0.1.5-pre) with a trailing 0x00, exactly as postcard::to_vec_cobs. */
+enum { RTW_MSG_IMAGE_START = 0, RTW_MSG_PIXEL = 1, RTW_MSG_IMAGE_END = 2 };
+typedef struct {
+  uint32_t kind;
+  uint32_t width, height, samples_per_pixel; /* RTW_MSG_IMAGE_START */
+  rtw_pixel pixel;                           /* RTW_MSG_PIXEL */
+} rtw_progress_msg;
+/* Encodes one message (<= 32 bytes incl. the 0x00 delimiter) into out; *len = bytes written. */
+int rtw_progress_encode(const rtw_progress_msg* msg, uint8_t* out, size_t cap, size_t* len);
+/* Decodes one COBS frame (with or without its trailing 0x00), as postcard::from_bytes_cobs. */
+int rtw_progress_decode(const uint8_t* frame, size_t len, rtw_progress_msg* msg);
+
 /* Render a subset of 8x8 pixel tiles into device memory (multi-GPU / framework path).
  * Tile t covers columns [8*tx, 8*tx+8) and output rows [8*ty, 8*ty+8) (row r <-> j = h-1-r),
  * tile id = ty * ceil(w/8) + tx.  If d_tile_ids == NULL all tiles are rendered and d_out is a

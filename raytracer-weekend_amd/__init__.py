@@ -65,6 +65,19 @@ class rtw_stats(C.Structure):
                                 for q, k in enumerate(("regen", "trace", "shade"))}}
 
 
+class rtw_pixel(C.Structure):  # lib.rs:120-126 Pixel
+    _fields_ = [("row", C.c_uint32), ("column", C.c_uint32), ("color", C.c_float * 3)]
+
+
+class rtw_progress_msg(C.Structure):  # lib.rs:128-138 ProgressMessage
+    _fields_ = [("kind", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("pixel", rtw_pixel)]
+
+
+MSG_IMAGE_START, MSG_PIXEL, MSG_IMAGE_END = 0, 1, 2
+PIXEL_SINK = C.CFUNCTYPE(C.c_int, C.POINTER(rtw_pixel), C.c_uint32, C.c_void_p)
+PIXEL_DTYPE = np.dtype([("row", np.uint32), ("column", np.uint32), ("color", np.float32, 3)])
+
 _F = C.POINTER(C.c_float)
 _U32 = C.POINTER(C.c_uint32)
 _U8 = C.POINTER(C.c_uint8)
@@ -106,6 +119,11 @@ _SIGS = {
                                     C.c_uint32, C.c_uint32, C.c_uint64, _U32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
     "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
+    "rtw_render_stream": (C.c_int, [C.c_void_p, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_uint64, C.c_uint32, PIXEL_SINK, C.c_void_p,
+                                    C.POINTER(rtw_stats)]),
+    "rtw_progress_encode": (C.c_int, [C.POINTER(rtw_progress_msg), _U8, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rtw_progress_decode": (C.c_int, [_U8, C.c_size_t, C.POINTER(rtw_progress_msg)]),
     "rtw_unpack_tiles_device": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
@@ -394,6 +412,29 @@ class Raytracer:
                                 self.max_depth, self.seed, out.ctypes.data_as(_F), C.byref(st)))
         return out, st.as_dict()
 
+    def render_stream(self, on_pixels, band_rows: int = 64):
+        """Raytracer::render() as a progressive Pixel stream (lib.rs:50-76): on_pixels(array of
+        PIXEL_DTYPE records) per finished band, in emission order (row j = h-1 .. 0).  -> stats."""
+        err = []
+
+        def sink(px, n, _user):
+            try:
+                buf = C.string_at(px, n * C.sizeof(rtw_pixel))
+                on_pixels(np.frombuffer(buf, PIXEL_DTYPE).copy())
+                return 0
+            except Exception as e:  # stop the render, re-raise below
+                err.append(e)
+                return RTW_ESTATE
+
+        cb = PIXEL_SINK(sink)
+        st = rtw_stats()
+        rc = lib().rtw_render_stream(self.scene._p, C.byref(self.cam.c), _fp(self.bg), self.w, self.h, self.spp,
+                                     self.max_depth, self.seed, band_rows, cb, None, C.byref(st))
+        if err:
+            raise err[0]
+        _check(rc)
+        return st.as_dict()
+
     def render_device(self, d_out_ptr: int, device: int = 0, d_tiles_ptr: int = 0, n_tiles: int = 0,
                       stream_ptr: int = 0, flags: int = 0, want_stats: bool = False):
         """Enqueue into device memory.  d_tiles_ptr: device uint32 tile ids (0 = whole image,
@@ -404,6 +445,31 @@ class Raytracer:
             self.seed, C.cast(C.c_void_p(d_tiles_ptr), _U32) if d_tiles_ptr else None, n_tiles,
             C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr), flags, C.byref(st) if want_stats else None))
         return st.as_dict() if want_stats else None
+
+
+def progress_encode(kind: int, width=0, height=0, spp=0, pixel=None) -> bytes:
+    """postcard::to_vec_cobs(&ProgressMessage) (lib.rs:128-138): COBS frame incl. its 0x00."""
+    m = rtw_progress_msg(kind=kind, width=width, height=height, samples_per_pixel=spp)
+    if pixel is not None:
+        m.pixel.row, m.pixel.column = int(pixel[0]), int(pixel[1])
+        m.pixel.color[:] = [float(x) for x in pixel[2]]
+    out = (C.c_uint8 * 64)()
+    n = C.c_size_t()
+    _check(lib().rtw_progress_encode(C.byref(m), out, 64, C.byref(n)))
+    return bytes(out[:n.value])
+
+
+def progress_decode(frame: bytes) -> dict:
+    """postcard::from_bytes_cobs::<ProgressMessage> (discovery_host_receiver/src/main.rs:37)."""
+    buf = (C.c_uint8 * max(1, len(frame))).from_buffer_copy(frame or b"\0")
+    m = rtw_progress_msg()
+    _check(lib().rtw_progress_decode(buf, len(frame), C.byref(m)))
+    d = {"kind": int(m.kind)}
+    if m.kind == MSG_IMAGE_START:
+        d.update(width=int(m.width), height=int(m.height), samples_per_pixel=int(m.samples_per_pixel))
+    elif m.kind == MSG_PIXEL:
+        d.update(row=int(m.pixel.row), column=int(m.pixel.column), color=[float(x) for x in m.pixel.color])
+    return d
 
 
 def perlin_generate(seed: int = 0):

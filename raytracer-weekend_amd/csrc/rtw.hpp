@@ -68,12 +68,22 @@ class World {
   TextureId checker(TextureId odd, TextureId even, float freq) { TextureId t; check(rtw_texture_checker(s_, odd, even, freq, &t)); return t; }
   TextureId image(const uint8_t* rgb, uint32_t w, uint32_t h) { TextureId t; check(rtw_texture_image(s_, rgb, w, h, &t)); return t; }
   TextureId uv_debug() { TextureId t; check(rtw_texture_uvdebug(s_, &t)); return t; }
+  // Noise::new(Perlin::new(rng), scale): Perlin tables from the build's seeded stream
+  TextureId noise(float scale, uint64_t perlin_seed) {
+    float g[768];
+    uint32_t p[768];
+    check(rtw_perlin_generate(perlin_seed, g, p));
+    TextureId t;
+    check(rtw_texture_noise(s_, g, p, scale, &t));
+    return t;
+  }
 
   MaterialId lambertian(TextureId t) { MaterialId m; check(rtw_material_lambertian(s_, t, &m)); return m; }
   MaterialId lambertian_solid(Color c) { return lambertian(solid_rgb(c.x, c.y, c.z)); }
   MaterialId metal(Color albedo, float fuzz) { MaterialId m; check(rtw_material_metal(s_, albedo.x, albedo.y, albedo.z, fuzz, &m)); return m; }
   MaterialId dielectric(float ir) { MaterialId m; check(rtw_material_dielectric(s_, ir, &m)); return m; }
   MaterialId diffuse_light(TextureId t) { MaterialId m; check(rtw_material_diffuse_light(s_, t, &m)); return m; }
+  MaterialId isotropic(TextureId t) { MaterialId m; check(rtw_material_isotropic(s_, t, &m)); return m; }
 
   void sphere(Point3 c, float r, MaterialId m) { check(rtw_add_spheres(s_, 1, &c.x, &c.y, &c.z, &r, &m)); }
   void moving_sphere(Point3 c0, float t0, Point3 c1, float t1, float r, MaterialId m) {
@@ -102,12 +112,26 @@ class World {
   template <class F> void bvh(float t0, float t1, F&& body) { check(rtw_begin_bvh(s_, t0, t1)); body(); check(rtw_end(s_)); }
   template <class F> void translate(Vec3 off, F&& body) { check(rtw_begin_translate(s_, off.x, off.y, off.z)); body(); check(rtw_end(s_)); }
   template <class F> void rotate_y(float deg, F&& body) { check(rtw_begin_rotate_y(s_, deg)); body(); check(rtw_end(s_)); }
+  // ConstantMedium::new(boundary, density, texture): body adds the boundary
+  template <class F> void constant_medium(float density, TextureId t, F&& body) {
+    check(rtw_begin_constant_medium(s_, density, t, nullptr)); body(); check(rtw_end(s_));
+  }
 
   // console_app/src/scenes.rs presets; returns the camera and background
   void preset(const std::string& name, float aspect, uint64_t seed, const std::string& models, Camera& cam, Color& bg) {
     float b[3];
     check(rtw_scene_preset(s_, name.c_str(), aspect, seed, models.c_str(), &cam.c, b));
     bg = Color{b[0], b[1], b[2]};
+  }
+  // every camera of a preset (animated-book2-final-scene has 30, scenes.rs:622-667)
+  static std::vector<Camera> preset_cameras(const std::string& name, float aspect, const std::string& models) {
+    uint32_t n = 0;
+    check(rtw_preset_cameras(name.c_str(), aspect, models.c_str(), nullptr, 0, &n));
+    std::vector<rtw_camera> raw(n);
+    check(rtw_preset_cameras(name.c_str(), aspect, models.c_str(), raw.data(), n, &n));
+    std::vector<Camera> out(n);
+    for (uint32_t k = 0; k < n; ++k) out[k].c = raw[k];
+    return out;
   }
   void commit(int device = -1) { check(rtw_scene_commit(s_, device)); }
 

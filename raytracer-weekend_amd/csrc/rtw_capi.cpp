@@ -444,6 +444,91 @@ int rtw_tonemap(const float* sum, uint32_t n, uint32_t spp, uint8_t* out) {
   return RTW_OK;
 }
 
+// ---------------------------------------------------------------- ProgressMessage wire format
+// postcard 0.7: varint (LEB128) u32 and enum tags, f32 little-endian; then COBS + 0x00.
+static void put_varint(std::vector<uint8_t>& o, uint32_t v) {
+  while (v >= 0x80) { o.push_back((uint8_t)(v | 0x80)); v >>= 7; }
+  o.push_back((uint8_t)v);
+}
+static void put_f32(std::vector<uint8_t>& o, float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  for (int k = 0; k < 4; ++k) o.push_back((uint8_t)(b >> (8 * k)));
+}
+int rtw_progress_encode(const rtw_progress_msg* m, uint8_t* out, size_t cap, size_t* len) {
+  if (!m || !len || (!out && cap)) return fail(RTW_EINVAL, "NULL argument");
+  std::vector<uint8_t> raw;
+  put_varint(raw, m->kind);
+  if (m->kind == RTW_MSG_IMAGE_START) {
+    put_varint(raw, m->width); put_varint(raw, m->height); put_varint(raw, m->samples_per_pixel);
+  } else if (m->kind == RTW_MSG_PIXEL) {
+    put_varint(raw, m->pixel.row); put_varint(raw, m->pixel.column);
+    for (int c = 0; c < 3; ++c) put_f32(raw, m->pixel.color[c]);
+  } else if (m->kind != RTW_MSG_IMAGE_END) {
+    return fail(RTW_EINVAL, "unknown ProgressMessage kind %u", m->kind);
+  }
+  // COBS: each block = (1 + run length of non-zero bytes, max 254) then the run
+  std::vector<uint8_t> enc(1, 0);
+  size_t code_at = 0;
+  uint8_t code = 1;
+  for (uint8_t b : raw) {
+    if (b == 0) {
+      enc[code_at] = code; code_at = enc.size(); enc.push_back(0); code = 1;
+    } else {
+      enc.push_back(b);
+      if (++code == 0xFF) { enc[code_at] = code; code_at = enc.size(); enc.push_back(0); code = 1; }
+    }
+  }
+  enc[code_at] = code;
+  enc.push_back(0);  // frame delimiter (to_vec_cobs)
+  *len = enc.size();
+  if (cap < enc.size()) return fail(RTW_EINVAL, "buffer too small (%zu < %zu)", cap, enc.size());
+  memcpy(out, enc.data(), enc.size());
+  return RTW_OK;
+}
+int rtw_progress_decode(const uint8_t* f, size_t n, rtw_progress_msg* m) {
+  if (!m || (!f && n)) return fail(RTW_EINVAL, "NULL argument");
+  if (n && f[n - 1] == 0) --n;
+  std::vector<uint8_t> raw;
+  for (size_t i = 0; i < n;) {  // COBS decode
+    const uint8_t code = f[i++];
+    if (code == 0) return fail(RTW_EIO, "COBS: zero byte inside a frame");
+    for (uint8_t k = 1; k < code; ++k) {
+      if (i >= n) return fail(RTW_EIO, "COBS: truncated block");
+      raw.push_back(f[i++]);
+    }
+    if (code != 0xFF && i < n) raw.push_back(0);
+  }
+  size_t at = 0;
+  auto varint = [&](uint32_t* v) -> bool {
+    uint32_t x = 0;
+    for (int sh = 0; sh < 35; sh += 7) {
+      if (at >= raw.size()) return false;
+      const uint8_t b = raw[at++];
+      x |= (uint32_t)(b & 0x7F) << sh;
+      if (!(b & 0x80)) { *v = x; return true; }
+    }
+    return false;
+  };
+  auto f32 = [&](float* v) -> bool {
+    if (at + 4 > raw.size()) return false;
+    uint32_t b = 0;
+    for (int k = 0; k < 4; ++k) b |= (uint32_t)raw[at++] << (8 * k);
+    memcpy(v, &b, 4);
+    return true;
+  };
+  memset(m, 0, sizeof *m);
+  if (!varint(&m->kind)) return fail(RTW_EIO, "postcard: unexpected end (DeserializeUnexpectedEnd)");
+  bool ok = true;
+  if (m->kind == RTW_MSG_IMAGE_START) ok = varint(&m->width) && varint(&m->height) && varint(&m->samples_per_pixel);
+  else if (m->kind == RTW_MSG_PIXEL)
+    ok = varint(&m->pixel.row) && varint(&m->pixel.column) && f32(&m->pixel.color[0]) && f32(&m->pixel.color[1]) &&
+         f32(&m->pixel.color[2]);
+  else if (m->kind != RTW_MSG_IMAGE_END) return fail(RTW_EIO, "postcard: bad enum tag %u", m->kind);
+  if (!ok) return fail(RTW_EIO, "postcard: unexpected end (DeserializeUnexpectedEnd)");
+  return RTW_OK;
+}
+
 // ---------------------------------------------------------------- introspection
 int rtw_scene_dump(const rtw_scene* s, char* buf, size_t cap, size_t* needed) {
   if (!s) return fail(RTW_EINVAL, "scene is NULL");

@@ -71,8 +71,10 @@ int main(int argc, char** argv) {
     else if (a == "--models") models = next("--models");
     else if (a == "--out") out_dir = next("--out");
     else if (a == "-h" || a == "--help") {
-      printf("usage: rtw_console <jumpy-balls|two-spheres|cornell-box|simple-triangle|wavefront-cow-obj|"
-             "textured-monument> [-w W] [-a ASPECT] [-s SPP] [--seed N] [--models DIR] [--out DIR]\n");
+      printf("usage: rtw_console <jumpy-balls|two-spheres|two-perlin-spheres|earth|simple-light|cornell-box|"
+             "smokey-cornell-box|book2-final-scene|animated-book2-final-scene|simple-triangle|wavefront-cow-obj|"
+             "wavefront-suspension-obj|textured-monument> [-w W] [-a ASPECT] [-s SPP] [--seed N] [--models DIR] "
+             "[--out DIR]\n");
       return 0;
     } else if (scene.empty()) scene = a;
     else { fprintf(stderr, "unexpected argument '%s'\n", a.c_str()); return 2; }
@@ -83,18 +85,24 @@ int main(int argc, char** argv) {
     rtw::World world;
     rtw::Camera cam;
     rtw::Color bg;
-    world.preset(scene, (float)width / (float)height, seed, models, cam, bg);
-    world.commit();
-    rtw::Raytracer rt(world, cam, bg, width, height, spp, seed);
-    rtw_stats st;
-    std::vector<float> sums = rt.render_sums(&st);
-    std::vector<uint8_t> img(sums.size());
-    rtw::check(rtw_tonemap(sums.data(), width * height, spp, img.data()));
+    const float cam_aspect = (float)width / (float)height;  // main.rs:38-41
+    world.preset(scene, cam_aspect, seed, models, cam, bg);
+    world.commit();  // flattened and uploaded once, reused by every camera (main.rs:47-56)
+    const std::vector<rtw::Camera> cams = rtw::World::preset_cameras(scene, cam_aspect, models);
     mkdir(out_dir.c_str(), 0755);
-    std::string path = out_dir + "/image_0000.png";
-    if (!write_png(path.c_str(), img.data(), width, height)) { fprintf(stderr, "cannot write %s\n", path.c_str()); return 1; }
-    printf("%s %ux%u %u spp: %.1f ms kernel, %llu rays, %.1f Mrays/s -> %s\n", scene.c_str(), width, height, spp,
-           st.kernel_ms, (unsigned long long)st.rays, st.rays / (st.kernel_ms * 1e3), path.c_str());
+    for (size_t frame = 0; frame < cams.size(); ++frame) {
+      rtw::Raytracer rt(world, cams[frame], bg, width, height, spp, seed);
+      rtw_stats st;
+      std::vector<float> sums = rt.render_sums(&st);
+      std::vector<uint8_t> img(sums.size());
+      rtw::check(rtw_tonemap(sums.data(), width * height, spp, img.data()));
+      char name[32];
+      snprintf(name, sizeof name, "/image_%04zu.png", frame);  // main.rs:92-94
+      std::string path = out_dir + name;
+      if (!write_png(path.c_str(), img.data(), width, height)) { fprintf(stderr, "cannot write %s\n", path.c_str()); return 1; }
+      printf("%s %ux%u %u spp: %.1f ms kernel, %llu rays, %.1f Mrays/s -> %s\n", scene.c_str(), width, height, spp,
+             st.kernel_ms, (unsigned long long)st.rays, st.rays / (st.kernel_ms * 1e3), path.c_str());
+    }
   } catch (const rtw::Error& e) {
     fprintf(stderr, "error %d: %s\n", e.code, e.what());
     return 1;

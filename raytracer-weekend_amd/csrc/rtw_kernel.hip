@@ -1288,6 +1288,74 @@ int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const flo
   return rc;
 }
 
+int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h, uint32_t spp,
+                      uint32_t max_depth, uint64_t seed, uint32_t band_rows, rtw_pixel_sink sink, void* user,
+                      rtw_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!s || !cam || !bg || !sink) return fail(RTW_EINVAL, "NULL argument");
+  if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
+  if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2 (lib.rs:84-85 divides by w-1, h-1)");
+  DeviceCopy* c = find_copy(s->s, -1);
+  if (!c) return fail(RTW_ENODEV, "scene has no device copy");
+  const uint32_t tiles_x = (w + 7u) / 8u, tiles_y = (h + 7u) / 8u;
+  const uint32_t band_ty = std::max(1u, ((band_rows ? band_rows : 64u) + 7u) / 8u);  // tile rows per band
+  int prev = 0;
+  hipGetDevice(&prev);
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  std::vector<uint32_t> ids((size_t)tiles_x * tiles_y);
+  for (uint32_t k = 0; k < ids.size(); ++k) ids[k] = k;  // tile row ty = output rows [8 ty, 8 ty + 8)
+  uint32_t* d_ids = nullptr;
+  float* d_packed = nullptr;
+  const size_t band_tiles = (size_t)band_ty * tiles_x;
+  int rc = RTW_OK;
+  if (hipMalloc((void**)&d_ids, ids.size() * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&d_packed, band_tiles * 64 * 3 * sizeof(float)) != hipSuccess) {
+    rc = fail(RTW_ENOMEM, "hipMalloc(stream buffers)");
+  } else if (hipMemcpy(d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    rc = fail(RTW_ENODEV, "hipMemcpy(tile ids)");
+  }
+  std::vector<float> packed(band_tiles * 64 * 3);
+  std::vector<rtw_pixel> px;
+  rtw_stats tot;
+  memset(&tot, 0, sizeof tot);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (uint32_t ty0 = 0; rc == RTW_OK && ty0 < tiles_y; ty0 += band_ty) {
+    const uint32_t nty = std::min(band_ty, tiles_y - ty0), nt = nty * tiles_x;
+    rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_ids + (size_t)ty0 * tiles_x, nt, d_packed, nullptr,
+                0, e0, e1);
+    rtw_stats st;
+    memset(&st, 0, sizeof st);
+    if (rc == RTW_OK) rc = fill_stats(*c, nullptr, e0, e1, 0, &st);
+    if (rc == RTW_OK && hipMemcpy(packed.data(), d_packed, (size_t)nt * 64 * 3 * sizeof(float),
+                                  hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(RTW_ENODEV, "hipMemcpy(band)");
+    if (rc != RTW_OK) break;
+    tot.rays += st.rays;
+    tot.kernel_ms += st.kernel_ms;
+    // emit rows of this band in reference order: output row r <-> j = h-1-r, columns 0..w-1
+    const uint32_t r0 = ty0 * 8u, r1 = std::min(h, (ty0 + nty) * 8u);
+    px.clear();
+    for (uint32_t r = r0; r < r1; ++r)
+      for (uint32_t i = 0; i < w; ++i) {
+        const size_t slot = (size_t)(r / 8u - ty0) * tiles_x + i / 8u, lane = (r % 8u) * 8u + (i % 8u);
+        const float* v = &packed[(slot * 64 + lane) * 3];
+        px.push_back(rtw_pixel{h - 1u - r, i, {v[0], v[1], v[2]}});
+      }
+    if (int e = sink(px.data(), (uint32_t)px.size(), user)) rc = e;
+  }
+  if (d_ids) hipFree(d_ids);
+  if (d_packed) hipFree(d_packed);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipSetDevice(prev);
+  tot.paths = (uint64_t)w * h * spp;
+  tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) *stats = tot;
+  return rc;
+}
+
 int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
   if (!s || (!ms && max_n)) return fail(RTW_EINVAL, "NULL argument");
   DeviceCopy* c = find_copy(s->s, device);
