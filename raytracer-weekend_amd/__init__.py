@@ -27,7 +27,7 @@ import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_ROOT = PKG_DIR.parent
-LIB_PATH = PKG_DIR / "lib" / "librtw_amd.so"
+LIB_PATH = Path(os.environ.get("RTW_LIB_PATH") or PKG_DIR / "lib" / "librtw_amd.so")  # override: tuning builds
 MODELS_DIR = REPO_ROOT / "models"
 
 RTW_EINVAL, RTW_ENOMEM, RTW_ENODEV, RTW_ESTATE, RTW_EIO = -22, -12, -19, -71, -5
