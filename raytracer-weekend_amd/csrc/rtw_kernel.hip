@@ -39,6 +39,9 @@ constexpr int BLOCK = 256;
 // (RenderArgs::spill).  STACK_LDS (33 rows) is for the 4-waves/SIMD tuning variants.
 constexpr int STACK_LDS = 32;
 constexpr int STACK_LDS5 = 24;
+// Deep-tree variants (mesh scenes): 31 rows x 256 lanes x 4 B x 5 blocks = 158,720 B <= 160 KiB, so a
+// push bound up to 30 (cow 25, monument 30) stays in LDS at 5 waves/SIMD without the spill path.
+constexpr int STACK_DEEP5 = 30;
 
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
@@ -1059,24 +1062,34 @@ static int env_int(const char* k, int dflt) {
   const char* e = getenv(k);
   return e ? atoi(e) : dflt;
 }
+struct Variant {
+  path_fn fn;
+  uint32_t stack;  // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
+};
 template <bool C, uint32_t F>
-static path_fn pick5(uint32_t need) {
+static Variant pick5(uint32_t need) {
   using namespace dev;
-  return need > (uint32_t)STACK_LDS5 ? path_kernel<C, STACK_LDS5, true, 5, F> : path_kernel<C, STACK_LDS5, false, 5, F>;
+  if (need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 5, F>, (uint32_t)STACK_LDS5};
+  if constexpr (F == F_MESHES || F == F_ALL) {
+    if (need <= (uint32_t)STACK_DEEP5) return {path_kernel<C, STACK_DEEP5, false, 5, F>, (uint32_t)STACK_DEEP5};
+    return {path_kernel<C, STACK_DEEP5, true, 5, F>, (uint32_t)STACK_DEEP5};
+  }
+  return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
 }
 template <bool C>
-static path_fn pick_kernel(uint32_t feat, uint32_t need) {
+static Variant pick_kernel(uint32_t feat, uint32_t need) {
   using namespace dev;
-  if (env_int("RTW_STACK_LDS", 0) == 4) return path_kernel<C, 4, true, 4, F_ALL>;  // spill-path test
+  if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
   switch (env_int("RTW_OCC", 5)) {
     case 4: {
       const bool sp = need > (uint32_t)STACK_LDS;
-      if (sph) return sp ? path_kernel<C, STACK_LDS, true, 4, F_SPHERES> : path_kernel<C, STACK_LDS, false, 4, F_SPHERES>;
-      return sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>;
+      const uint32_t st = (uint32_t)STACK_LDS;
+      if (sph) return {sp ? path_kernel<C, STACK_LDS, true, 4, F_SPHERES> : path_kernel<C, STACK_LDS, false, 4, F_SPHERES>, st};
+      return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
     case 6:
-      if (sph && need <= (uint32_t)STACK_LDS5) return path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>;
+      if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
       [[fallthrough]];
     default:
       if (env_int("RTW_GENERIC", 0)) return pick5<C, F_ALL>(need);  // parity of the generic kernel
@@ -1087,12 +1100,7 @@ static path_fn pick_kernel(uint32_t feat, uint32_t need) {
       return pick5<C, F_ALL>(need);
   }
 }
-static uint32_t stack_lds(uint32_t feat, uint32_t need) {
-  (void)feat; (void)need;
-  if (env_int("RTW_STACK_LDS", 0) == 4) return 4;
-  return env_int("RTW_OCC", 5) == 4 ? dev::STACK_LDS : dev::STACK_LDS5;
-}
-static path_fn path_kernel_ptr(bool count, uint32_t feat, uint32_t need) {
+static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need) {
   return count ? pick_kernel<true>(feat, need) : pick_kernel<false>(feat, need);
 }
 
@@ -1158,9 +1166,10 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const path_fn fn = path_kernel_ptr(count, sc.flat.features, sc.flat.stack_need);
+    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need);
+    const path_fn fn = var.fn;
     const int grid = resident_grid(c, fn, count);
-    const uint32_t lds = stack_lds(sc.flat.features, sc.flat.stack_need);
+    const uint32_t lds = var.stack;
     a.spill_depth = sc.flat.stack_need > lds ? sc.flat.stack_need - lds : 0;
     a.spill_lanes = (uint32_t)grid * dev::BLOCK;
     const size_t spill_bytes = (size_t)a.spill_depth * a.spill_lanes * sizeof(int32_t);
