@@ -1049,7 +1049,14 @@ static DeviceCopy* find_copy(Scene& s, int device) {
   return nullptr;
 }
 
-constexpr uint64_t MAX_PASS_PATHS = 1ull << 30;  // 12.9 GB of ordered samples per pass
+// Paths per pass (ordered sample buffer = 12 B per path): 2^32 = 51.5 GB of the 288 GB HBM.  A frame
+// with more paths (monument 4K x 1024 spp: 8.5 G, 2 passes) runs in several passes, each one persistent
+// launch + its in-order reduction.  Tuning knob RTW_PASS_LOG2 (24..33).
+static uint64_t max_pass_paths() {
+  const char* e = getenv("RTW_PASS_LOG2");
+  const int l = e ? std::min(33, std::max(24, atoi(e))) : 32;
+  return 1ull << l;
+}
 
 // Variants of the path kernel: feature set x the waves per SIMD the register allocator must allow.
 // Sphere-only scenes (jumpy-balls) get the specialised kernel; everything else the generic one.
@@ -1155,7 +1162,7 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
   } else if (n_slots) {
     const uint64_t per_slot = 64ull * spp;
-    const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, MAX_PASS_PATHS / per_slot);
+    const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, max_pass_paths() / per_slot);
     const uint64_t need = std::min<uint64_t>(n_slots, slots_per_pass) * per_slot;
     if (need > c.sbuf_paths) {  // grow the ordered sample buffer (first render only)
       if (c.sbuf) HIPCHK(hipFree(c.sbuf), "hipFree(sample buffer)");
