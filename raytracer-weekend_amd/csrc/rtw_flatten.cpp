@@ -14,6 +14,7 @@
 // the BVH and tested for every ray ("always" list): it keeps the tree tight and removes
 // the grazing-ray precision cases of a 1000-unit sphere from the culling argument.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -289,8 +290,19 @@ struct Builder {
 };
 
 // ---------------------------------------------------------------- binned SAH BVH2
-constexpr int LEAF_MAX = 4;
-constexpr int NBINS = 16;
+// Build parameters (tuning knobs RTW_BVH_LEAF 1..7, RTW_BVH_TRAV = SAH cost of a BVH2 traversal step
+// relative to one primitive test, RTW_BVH_BINS 4..64)
+struct BuildParams {
+  int leaf_max = 4;
+  float trav = 0.5f;
+  int bins = 16;
+  BuildParams() {
+    if (const char* e = getenv("RTW_BVH_LEAF")) leaf_max = std::min(7, std::max(1, atoi(e)));
+    if (const char* e = getenv("RTW_BVH_TRAV")) trav = (float)atof(e);
+    if (const char* e = getenv("RTW_BVH_BINS")) bins = std::min(64, std::max(4, atoi(e)));
+  }
+};
+constexpr int NBINS_MAX = 64;
 constexpr uint32_t MAX_DEPTH = 31;  // the kernel's traversal stack holds 32 entries
 
 struct Ref {
@@ -303,6 +315,7 @@ struct BvhBuild {
   std::vector<Leaf>& L;
   std::vector<DevNode>& nodes;
   uint32_t median_depth;  // from here on: median splits, so depth <= MAX_DEPTH
+  BuildParams P;
   uint32_t max_depth = 0;
 
   Ref build(uint32_t b, uint32_t e, uint32_t depth) {
@@ -320,16 +333,17 @@ struct BvhBuild {
       for (int a = 0; a < 3; ++a) {
         float lo = cbox.lo[a], hi = cbox.hi[a];
         if (!(hi > lo)) continue;
-        Box bb[NBINS];
-        uint32_t cnt[NBINS] = {0};
+        Box bb[NBINS_MAX];
+        uint32_t cnt[NBINS_MAX] = {0};
+        const int NBINS = P.bins;
         float sc = NBINS / (hi - lo);
         for (uint32_t k = b; k < e; ++k) {
           int bi = std::min(NBINS - 1, (int)((L[k].c[a] - lo) * sc));
           cnt[bi]++;
           bb[bi].grow(L[k].wbox);
         }
-        Box left[NBINS];
-        uint32_t lc[NBINS];
+        Box left[NBINS_MAX];
+        uint32_t lc[NBINS_MAX];
         Box acc;
         uint32_t c = 0;
         for (int q = 0; q < NBINS; ++q) { acc.grow(bb[q]); c += cnt[q]; left[q] = acc; lc[q] = c; }
@@ -344,12 +358,13 @@ struct BvhBuild {
         }
       }
       float leaf_cost = box.area() * n;
-      float split_cost = box.area() * 0.5f + best_cost;  // traversal ~ half a prim test
-      if (n <= LEAF_MAX && (best_axis < 0 || split_cost >= leaf_cost))
+      float split_cost = box.area() * P.trav + best_cost;  // traversal step vs prim test
+      if (n <= (uint32_t)P.leaf_max && (best_axis < 0 || split_cost >= leaf_cost))
         return Ref{box, (int32_t)b, n};
     }
     uint32_t mid;
     if (best_axis >= 0) {
+      const int NBINS = P.bins;
       float lo = cbox.lo[best_axis], sc = NBINS / (cbox.hi[best_axis] - lo);
       auto it = std::partition(L.begin() + b, L.begin() + e, [&](const Leaf& x) {
         return std::min(NBINS - 1, (int)((x.c[best_axis] - lo) * sc)) < best_bin;
