@@ -263,6 +263,13 @@ def main() -> int:
         d = json.loads(tj.read_text())
         if d.get("launches_per_frame", 1) == launches and d.get("world", 1) == world:
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(ROOT))
+    # what does bound it: SQ counters of the same config (scripts/gpu_counters.sh + valu_summary.py)
+    issue = None
+    vj = ROOT / "profiles" / f"valu_{args.config}.json"
+    if vj.exists() and not args.spp:
+        d = json.loads(vj.read_text())
+        issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit")}
+        issue["source"] = str(vj.relative_to(ROOT))
 
     out = None
     if rank == 0:
@@ -284,7 +291,7 @@ def main() -> int:
                        "tiles": nt, "launches_per_frame": launches, "parallelism": f"tiles{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": traffic_src, "kernel": "path_kernel",
+                         "traffic_source": traffic_src, "issue_counters": issue, "kernel": "path_kernel",
                          "kernel_ms_per_frame": round(frame_kernel_ms, 3),
                          "kernel_launches_per_frame": launches * passes,
                          "alg_bytes_per_launch": round(alg_bytes_rank / (launches * passes)),

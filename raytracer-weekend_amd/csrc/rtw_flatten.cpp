@@ -181,9 +181,13 @@ struct Builder {
         DevPrim p;
         memset(&p, 0, sizeof p);
         p.type_inst = PT_MSPHERE;
+        // q0 = (c0, t0), q1 = (c1 - c0, t1), q2 = (r, r * r): the f32 subtraction and product the
+        // reference evaluates per call (spherical.rs:29, :117-123), done once here (same IEEE ops)
         memcpy(p.q0, n.f, 4 * sizeof(float));
-        memcpy(p.q1, n.f + 4, 4 * sizeof(float));
+        for (int a = 0; a < 3; ++a) p.q1[a] = n.f[4 + a] - n.f[a];
+        p.q1[3] = n.f[7];
         p.q2[0] = n.f[8];
+        p.q2[1] = n.f[8] * n.f[8];
         p.mat = n.mat;
         float r = fabsf(n.f[8]);
         Box b;

@@ -232,11 +232,12 @@ __device__ __forceinline__ Ray to_local(const DevInst* in, Ray r) {
 }
 
 // ---- candidate t of one primitive (independent of t_max; -1 = miss)
-__device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad) {  // spherical.rs:26-44
+// rad2 = radius * radius (precomputed for moving spheres; the same f32 product)
+__device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad2) {  // spherical.rs:26-44
   V3 oc = sub(r.o, c);
   float a = len2(r.d);
   float hb = dot(oc, r.d);
-  float cc = len2(oc) - rad * rad;
+  float cc = len2(oc) - rad2;
   float disc = hb * hb - a * cc;
   if (!(disc >= 0.0f)) return -1.0f;
   float sq = sqrtf(disc);
@@ -244,9 +245,13 @@ __device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad) {  /
   if (root < TMIN) root = (-hb + sq) / a;  // root1 > t_max implies root2 > t_max
   return root;
 }
-__device__ __forceinline__ V3 center_at(const float* q0, const float* q1, float time) {  // :117-123
-  V3 c0 = ld3(q0), c1 = ld3(q1);
-  return add(c0, scale(sub(c1, c0), (time - q0[3]) / (q1[3] - q0[3])));
+// spherical.rs:117-123 over the flattened layout q0 = (c0, t0), q1 = (c1 - c0, t1) (rtw_flatten.cpp).
+// For the shutter [+0, 1] the fraction (time - 0) / (1 - 0) is `time` exactly: the IEEE division
+// is skipped (a wave-uniform branch in practice: every moving sphere of a scene shares it).
+__device__ __forceinline__ V3 center_at(const float* q0, const float* q1, float time) {
+  float frac = time;
+  if (__float_as_uint(q0[3]) != 0u || q1[3] != 1.0f) frac = (time - q0[3]) / (q1[3] - q0[3]);
+  return add(ld3(q0), scale(ld3(q1), frac));
 }
 template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
 __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float k) {
@@ -379,12 +384,11 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
   float t = -1.0f;
   if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
-    t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3]);
+    t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3] * q0[3]);
   } else if ((FEAT & F_MSPHERE) && type == PT_MSPHERE) {
     const float4 q1v = P[1];
     const float q1[4] = {q1v.x, q1v.y, q1v.z, q1v.w};
-    const float rad = P[2].x;
-    t = cand_sphere(lr, center_at(q0, q1, lr.time), rad);
+    t = cand_sphere(lr, center_at(q0, q1, lr.time), P[2].y);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float4 q1v = P[1], q2v = P[2];
     const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
@@ -866,40 +870,42 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     } else {
       const Rec h = hit_record<FEAT>(S, st.ray, b);
       const DevMat& m = S.mats[h.mat];
-      if ((FEAT & F_LIGHT) && m.type == MT_LIGHT) {  // light_source.rs:17-24: emit, no scatter
-        L = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
+      // One body for every material (material.rs:42-165, light_source.rs:17-24): a wave mixing
+      // materials runs the rejection loop, unit() and the texture lookup once instead of once per
+      // material branch.  Each material's draws and f32 operations are unchanged.
+      const uint32_t mt = m.type;
+      const bool light = (FEAT & F_LIGHT) && mt == MT_LIGHT;
+      const bool lam = (FEAT & F_LAMBERT) && mt == MT_LAMBERT;
+      const bool met = (FEAT & F_METAL) && mt == MT_METAL;
+      const bool iso = (FEAT & F_ISO) && mt == MT_ISOTROPIC;
+      V3 rs = mk(0.f, 0.f, 0.f);
+      if (lam || met || iso) rs = rand_in_unit_sphere(st.rng);  // vec3.rs:101-108
+      const V3 ud = unit(lam ? rs : st.ray.d);                  // Lambertian: unit(rs); else unit(d_in)
+      V3 att = mk(1.f, 1.f, 1.f);                                 // Dielectric: attenuation (1,1,1)
+      if (met) att = ld3(m.albedo);
+      else if (light || lam || iso) att = tex_value<FEAT>(S, m.tex, h.u, h.v, h.p);
+      if (light) {  // emit, no scatter
+        L = mul(st.T, att);
         done = true;
-      } else if ((FEAT & F_LAMBERT) && m.type == MT_LAMBERT) {  // material.rs:42-56
-        V3 dir = add(h.n, unit(rand_in_unit_sphere(st.rng)));
-        if (near_zero(dir)) dir = h.n;
-        st.T = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
+      } else {
+        V3 dir = rs;  // Isotropic (material.rs:155-165): never absorbs
+        if (lam) {    // material.rs:42-56
+          dir = add(h.n, ud);
+          if (near_zero(dir)) dir = h.n;
+        } else if (met) {  // material.rs:78-95
+          dir = add(reflect(ud, h.n), scale(rs, m.param));
+          done = !(dot(dir, h.n) > 0.0f);  // absorbed: emitted() is black
+        } else if (!iso && (FEAT & F_DIEL)) {  // Dielectric, material.rs:116-142
+          const float ratio = h.front ? 1.0f / m.param : m.param;
+          const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
+          const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+          const bool cannot = (ratio * sin_t) > 1.0f;
+          if (cannot || reflectance(cos_t, ratio) > gen_f32(st.rng)) dir = reflect(ud, h.n);
+          else dir = refract(ud, h.n, ratio);
+        }
+        st.T = mul(st.T, att);  // x * 1.0f == x: the Dielectric's T is unchanged
         st.ray.o = h.p;
         st.ray.d = dir;
-      } else if ((FEAT & F_METAL) && m.type == MT_METAL) {  // material.rs:78-95
-        V3 refl = reflect(unit(st.ray.d), h.n);
-        V3 dir = add(refl, scale(rand_in_unit_sphere(st.rng), m.param));
-        if (dot(dir, h.n) > 0.0f) {
-          st.T = mul(st.T, ld3(m.albedo));
-          st.ray.o = h.p;
-          st.ray.d = dir;
-        } else {
-          done = true;  // absorbed: emitted() is black
-        }
-      } else if ((FEAT & F_ISO) && m.type == MT_ISOTROPIC) {  // material.rs:155-165, never absorbs
-        st.T = mul(st.T, tex_value<FEAT>(S, m.tex, h.u, h.v, h.p));
-        st.ray.o = h.p;
-        st.ray.d = rand_in_unit_sphere(st.rng);
-      } else if (FEAT & F_DIEL) {  // Dielectric, material.rs:116-142
-        const float ratio = h.front ? 1.0f / m.param : m.param;
-        const V3 ud = unit(st.ray.d);
-        const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
-        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
-        const bool cannot = (ratio * sin_t) > 1.0f;
-        V3 dir;
-        if (cannot || reflectance(cos_t, ratio) > gen_f32(st.rng)) dir = reflect(ud, h.n);
-        else dir = refract(ud, h.n, ratio);
-        st.ray.o = h.p;
-        st.ray.d = dir;  // attenuation (1,1,1): T unchanged
       }
       if (!done && --st.depth == 0) done = true;  // lib.rs:98-100: depth 0 returns black
     }
