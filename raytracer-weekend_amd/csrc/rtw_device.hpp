@@ -150,6 +150,7 @@ struct RenderArgs {
   uint32_t tiles_x;           // ceil(w / 8)
   uint32_t slot_base;         // first tile slot of this pass
   uint32_t quota16;           // trace_run returns once quota16/16 of the wave's lanes are done
+  uint32_t regen_min;         // regenerate once this many lanes are idle (or every lane is)
   const uint32_t* tile_ids;   // device array or nullptr (slot == tile id, full-image output)
   uint64_t seed_hash;         // splitmix64(seed)
   uint64_t n_paths;           // paths in this pass = slots * 64 * spp
