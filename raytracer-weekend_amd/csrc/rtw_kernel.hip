@@ -753,12 +753,22 @@ struct PathState {
   uint32_t depth;
 };
 
+// floor(n / d) for 32-bit n and d >= 2 from M = UINT64_MAX / d + 1 (Lemire, Kaser & Kurz 2019,
+// "Faster remainder by direct computation"): hi64(M * n) in two 32-bit multiplies instead of the
+// ~25-instruction runtime u32 division; checked exhaustively for 12 divisors over every n and for
+// 1e8 random pairs on the host.
+__device__ __forceinline__ uint32_t fastdiv(uint32_t n, uint64_t M) {
+  const uint64_t t = (uint64_t)(uint32_t)(M >> 32) * n + __umulhi((uint32_t)M, n);
+  return (uint32_t)(t >> 32);
+}
+
 __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
-  const uint32_t slot = hi / a.spp, s = hi - slot * a.spp;
+  const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
   const uint32_t gslot = a.slot_base + slot;
   const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
-  const uint32_t i = (tile % a.tiles_x) * 8u + (l & 7u), row = (tile / a.tiles_x) * 8u + (l >> 3);
+  const uint32_t ty = a.tiles_x > 1u ? fastdiv(tile, a.tiles_x_magic) : tile;
+  const uint32_t i = (tile - ty * a.tiles_x) * 8u + (l & 7u), row = ty * 8u + (l >> 3);
   if (i >= a.w || row >= a.h) return false;
   const uint32_t j = a.h - 1u - row;
   const DevCamera& C = a.cam;
@@ -1150,6 +1160,8 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   memcpy(a.bg, bg, sizeof a.bg);
   a.w = w; a.h = h; a.spp = spp; a.max_depth = max_depth;
   a.tiles_x = (w + 7u) / 8u;
+  a.spp_magic = spp > 1u ? UINT64_MAX / spp + 1u : 0u;
+  a.tiles_x_magic = a.tiles_x > 1u ? UINT64_MAX / a.tiles_x + 1u : 0u;
   a.tile_ids = d_tiles;
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
   if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));

@@ -112,6 +112,19 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
 
 
+@pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16"])
+def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
+    """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
+    yields (quota16) change only which lanes run which path when; every path's draws and
+    operations are keyed by its (pixel, sample) id, so the image and the ray count must not move."""
+    k, v = knob.split("=")
+    monkeypatch.setenv(k, v)
+    for name, aspect, w, h, spp in (SCENES[0], SCENES[1]):
+        g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
+        assert st["rays"] == rays
+        assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
+
+
 def test_path_kernel_times(gpu):
     rtw = gpu
     s = rtw.Scene()
