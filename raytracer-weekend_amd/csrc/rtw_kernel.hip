@@ -371,16 +371,17 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
   }
 }
 
-template <bool COUNT, uint32_t FEAT>
+// LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
+template <bool COUNT, uint32_t FEAT, bool LOCAL = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
                                           uint32_t* cnt, uint64_t seg) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
   const float4 q0v = P[0];
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
-  // object-space ray of the prim's wrapper chain; recomputed per test (a few flops) rather than
-  // cached, which keeps 8 VGPRs free for occupancy
-  const Ray lr = ((FEAT & F_INST) && inst) ? to_local(S.insts + inst, wr) : wr;
+  // object-space ray of the prim's wrapper chain; in BVH leaves recomputed per test (a few
+  // flops) rather than cached, which keeps 8 VGPRs free for occupancy
+  const Ray lr = (!LOCAL && (FEAT & F_INST) && inst) ? to_local(S.insts + inst, wr) : wr;
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
   float t = -1.0f;
   if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
@@ -437,7 +438,23 @@ template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
                                             uint64_t seg) {
   ts.b = Best{INFINITY, 0u, -1};
-  for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt, seg);
+  if (FEAT & F_INST) {
+    // the always list is wave-uniform and in DFS order, so a wrapper chain's prims are adjacent
+    // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
+    uint32_t cur = 0;
+    Ray lr = r;
+    for (uint32_t k = 0; k < S.n_always; ++k) {
+      const uint32_t pi = S.always[k];
+      const uint32_t inst = S.prims[pi].type_inst >> 8;
+      if (inst != cur) {
+        lr = inst ? to_local(S.insts + inst, r) : r;
+        cur = inst;
+      }
+      test_prim<COUNT, FEAT, true>(S, pi, lr, ts.b, cnt, seg);
+    }
+  } else {
+    for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT>(S, S.always[k], r, ts.b, cnt, seg);
+  }
   ts.node = S.n_nodes ? 0 : -1;
   ts.pend = 0;
   ts.sp = 0;

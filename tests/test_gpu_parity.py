@@ -112,11 +112,14 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
 
 
-@pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16"])
+@pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16",
+                                  "RTW_LIST_MAX=0", "RTW_LIST_MAX=64"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
-    operations are keyed by its (pixel, sample) id, so the image and the ray count must not move."""
+    operations are keyed by its (pixel, sample) id, so the image and the ray count must not move.
+    Same for list mode vs BVH (RTW_LIST_MAX): closest hit with ties to the later object is a
+    commutative reduction over the leaves, whatever culls them."""
     k, v = knob.split("=")
     monkeypatch.setenv(k, v)
     for name, aspect, w, h, spp in (SCENES[0], SCENES[1]):
