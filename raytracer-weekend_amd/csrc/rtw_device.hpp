@@ -116,6 +116,9 @@ enum Feature : uint32_t {
   F_ISO = 1u << 15,     // Isotropic materials
 };
 constexpr uint32_t F_ALL = (1u << 16) - 1;
+// Kernel-only flag (not a scene feature): the world has no BVH (list mode, rtw_flatten.cpp), so
+// the variant compiles without the BVH walk and its registers (higher occupancy).
+constexpr uint32_t F_LIST = 1u << 16;
 // Kernel variants (the smallest superset of a scene's features is launched): sphere worlds
 // (jumpy-balls), rect/instance worlds with solid colours (cornell-box), the same with media
 // (smokey-cornell-box), diffuse meshes (cow, monument), and everything.

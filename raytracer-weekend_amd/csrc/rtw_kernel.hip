@@ -880,9 +880,12 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       ++nrays;
       trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     }
-    {
+    if (!(FEAT & F_LIST)) {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng);
+    } else {
+      ts.node = -1;  // list mode: trace_begin tested every primitive
+      ts.sp = 0;
     }
     phase(1);
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
@@ -1117,10 +1120,20 @@ static Variant pick5(uint32_t need) {
   return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
 }
 template <bool C>
-static Variant pick_kernel(uint32_t feat, uint32_t need) {
+static Variant pick_kernel(uint32_t feat, uint32_t need, bool list) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
+  if (list && !env_int("RTW_GENERIC", 0)) {
+    // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
+    // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
+    // at 8; knob RTW_LIST_OCC); the all-features one spills below 96 VGPRs, so it stays at 5.
+    if ((feat & ~F_BOXES) == 0) {
+      if (env_int("RTW_LIST_OCC", 8) == 6) return {path_kernel<C, 1, false, 6, F_BOXES | F_LIST>, 1u};
+      return {path_kernel<C, 1, false, 8, F_BOXES | F_LIST>, 1u};
+    }
+    return {path_kernel<C, 1, false, 5, F_ALL | F_LIST>, 1u};
+  }
   switch (env_int("RTW_OCC", 5)) {
     case 4: {
       const bool sp = need > (uint32_t)STACK_LDS;
@@ -1140,8 +1153,8 @@ static Variant pick_kernel(uint32_t feat, uint32_t need) {
       return pick5<C, F_ALL>(need);
   }
 }
-static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need) {
-  return count ? pick_kernel<true>(feat, need) : pick_kernel<false>(feat, need);
+static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need, bool list) {
+  return count ? pick_kernel<true>(feat, need, list) : pick_kernel<false>(feat, need, list);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, bool count) {
@@ -1208,7 +1221,7 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need);
+    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need, sc.flat.nodes4.empty());
     const path_fn fn = var.fn;
     // Regenerate paths only once >= regen_min lanes of a wave are idle (or all are): start_path
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
