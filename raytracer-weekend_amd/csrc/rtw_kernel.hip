@@ -766,7 +766,7 @@ struct PathState {
   Ray ray;
   V3 T;
   uint64_t rng;
-  uint64_t pid;
+  uint32_t pid;  // path id within the pass (a pass holds at most 2^32 paths, max_pass_paths)
   uint32_t depth;
 };
 
@@ -802,7 +802,7 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   st.rng = rng;
   st.T = mk(1.f, 1.f, 1.f);
   st.depth = a.max_depth;
-  st.pid = pid;
+  st.pid = (uint32_t)pid;
   return true;
 }
 
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (done) {
       a.sbuf[st.pid] = L.x;
       a.sbuf[P + st.pid] = L.y;
-      a.sbuf[2 * P + st.pid] = L.z;
+      a.sbuf[2 * P + (uint64_t)st.pid] = L.z;
       has = false;
     }
   }
@@ -1090,7 +1090,7 @@ static DeviceCopy* find_copy(Scene& s, int device) {
 // launch + its in-order reduction.  Tuning knob RTW_PASS_LOG2 (24..33).
 static uint64_t max_pass_paths() {
   const char* e = getenv("RTW_PASS_LOG2");
-  const int l = e ? std::min(33, std::max(24, atoi(e))) : 32;
+  const int l = e ? std::min(32, std::max(24, atoi(e))) : 32;  // PathState::pid is 32-bit
   return 1ull << l;
 }
 
