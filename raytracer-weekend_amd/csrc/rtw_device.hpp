@@ -159,7 +159,7 @@ struct RenderArgs {
   const uint32_t* tile_ids;   // device array or nullptr (slot == tile id, full-image output)
   uint64_t seed_hash;         // splitmix64(seed)
   uint64_t n_paths;           // paths in this pass = slots * 64 * spp
-  float* sbuf;                // ordered sample buffer: 3 planes of n_paths floats
+  float* sbuf;                // ordered sample buffer: n_paths x (r, g, b) floats, path-major
   float* out;
   unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
   unsigned long long* queue;     // path-id dispenser of this pass

@@ -940,9 +940,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       if (!done && --st.depth == 0) done = true;  // lib.rs:98-100: depth 0 returns black
     }
     if (done) {
-      a.sbuf[st.pid] = L.x;
-      a.sbuf[P + st.pid] = L.y;
-      a.sbuf[2 * P + (uint64_t)st.pid] = L.z;
+      float* o = a.sbuf + (size_t)st.pid * 3u;  // one path's 12 B share a cache line
+      o[0] = L.x;
+      o[1] = L.y;
+      o[2] = L.z;
       has = false;
     }
   }
@@ -971,13 +972,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
   const uint32_t i = (tile % a.tiles_x) * 8u + (l & 7u), row = (tile / a.tiles_x) * 8u + (l >> 3);
   if (i >= a.w || row >= a.h) return;
-  const uint64_t P = a.n_paths;
   float x = 0.f, y = 0.f, z = 0.f;
-  uint64_t idx = (uint64_t)slot * a.spp * 64u + l;
-  for (uint32_t s = 0; s < a.spp; ++s, idx += 64u) {
-    x = x + a.sbuf[idx];
-    y = y + a.sbuf[P + idx];
-    z = z + a.sbuf[2 * P + idx];
+  const float* q = a.sbuf + ((size_t)slot * a.spp * 64u + l) * 3u;
+  for (uint32_t s = 0; s < a.spp; ++s, q += 64u * 3u) {
+    x = x + q[0];
+    y = y + q[1];
+    z = z + q[2];
   }
   float* o = a.tile_ids ? a.out + ((size_t)gslot * 64u + l) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
   o[0] = x;

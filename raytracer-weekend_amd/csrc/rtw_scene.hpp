@@ -76,7 +76,7 @@ struct DeviceCopy {
   size_t bytes = 0;
   DevScene scene{};
   unsigned long long* counters = nullptr;  // 32 x u64: [0..19] stats, [31] path queue
-  float* sbuf = nullptr;                   // ordered per-sample radiance (3 planes)
+  float* sbuf = nullptr;                   // ordered per-sample radiance (rgb per path)
   uint64_t sbuf_paths = 0;
   int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)
   size_t spill_bytes = 0;
