@@ -86,8 +86,8 @@ __device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
 __device__ __forceinline__ float gen_f32(uint64_t& s) {  // rand Standard<f32>
   return (float)(pcg_next(s) >> 8) * (1.0f / 16777216.0f);
 }
-__device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi) {  // UniformFloat::sample_single
-  float sc = hi - lo;
+__device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi, float sc) {
+  // UniformFloat::sample_single with sc = hi - lo precomputed (kernel-uniform: stays in an SGPR)
   for (;;) {
     float v01 = __uint_as_float((pcg_next(s) >> 9) | 0x3F800000u) - 1.0f;
     float r = v01 * sc + lo;
@@ -779,6 +779,15 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t n, uint64_t M) {
   return (uint32_t)(t >> 32);
 }
 
+// readfirstlane of a 64-bit value.  The builtin returns a signed int: each half must go through
+// uint32_t before widening, or a low half >= 2^31 sign-extends over the high half (path ids of a
+// pass above 2^31 — monument-4k's 2^32-path passes — became huge and wrote outside the buffer).
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
   const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
@@ -791,14 +800,14 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   const DevCamera& C = a.cam;
   uint64_t rng = splitmix64(splitmix64(a.seed_hash ^ (((uint64_t)j << 32) | i)) ^ (uint64_t)s);
   // lib.rs:84-86 + camera.rs:66-74
-  const float u = ((float)i + gen_f32(rng)) / (float)(a.w - 1u);
-  const float v = ((float)j + gen_f32(rng)) / (float)(a.h - 1u);
+  const float u = ((float)i + gen_f32(rng)) / a.fw1;
+  const float v = ((float)j + gen_f32(rng)) / a.fh1;
   const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
   const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
   st.ray.o = add(ld3(C.origin), off);
   st.ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)), ld3(C.origin)),
                  off);
-  st.ray.time = gen_range(rng, C.time0, C.time1);
+  st.ray.time = gen_range(rng, C.time0, C.time1, a.time_span);
   st.rng = rng;
   st.T = mk(1.f, 1.f, 1.f);
   st.depth = a.max_depth;
@@ -850,6 +859,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(a.queue, (unsigned long long)BATCH);
         b = __shfl(b, 0, 64);
+        // wave-uniform: keep the pool bounds in SGPRs (frees VGPRs the allocator otherwise spills)
+        b = rfl64(b);
         if (b < P) {
           nb = b;
           ne = b + BATCH < P ? b + BATCH : P;
@@ -868,18 +879,20 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
         pool_end = ne;
         if (pool_next > pool_end) pool_next = pool_end;
       }
+      pool_next = rfl64(pool_next);  // uniform by construction; tell the register allocator
+      pool_end = rfl64(pool_end);
     }
     if (__ballot(has) == 0) {
       if (exhausted) break;
       continue;  // every id handed out this round was an off-image pixel: draw again
     }
     phase(0);
+    // segments starting now, counted per wave with every lane active (so the count is uniform
+    // and stays in SGPRs)
+    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
-    if (!ts.on) {
-      ++nrays;
-      trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
-    }
+    if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     if (!(FEAT & F_LIST)) {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng);
@@ -947,9 +960,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       has = false;
     }
   }
-  unsigned long long tot = nrays;
-  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
-  if (lane == 0 && tot) atomicAdd(a.counters, tot);
+  if (lane == 0 && nrays) atomicAdd(a.counters, nrays);  // nrays counts the whole wave's segments
   if (COUNT) {
     phase(2);
     if (lane == 0) {
@@ -1134,7 +1145,9 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list) {
     }
     return {path_kernel<C, 1, false, 5, F_ALL | F_LIST>, 1u};
   }
-  switch (env_int("RTW_OCC", 5)) {
+  // sphere worlds default to 6 waves/SIMD (24 B/lane of register spill, +1.6% on jumpy-balls over
+  // 5 waves once the kernel-uniform values left the VGPRs); the other variants to 5
+  switch (env_int("RTW_OCC", sph ? 6 : 5)) {
     case 4: {
       const bool sp = need > (uint32_t)STACK_LDS;
       const uint32_t st = (uint32_t)STACK_LDS;
@@ -1191,6 +1204,12 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   a.w = w; a.h = h; a.spp = spp; a.max_depth = max_depth;
   a.tiles_x = (w + 7u) / 8u;
   a.spp_magic = spp > 1u ? UINT64_MAX / spp + 1u : 0u;
+  a.fw1 = (float)(w - 1u);
+  a.fh1 = (float)(h - 1u);
+  {
+    volatile float t0 = cam->time0, t1 = cam->time1;  // one IEEE f32 subtraction, as on the device
+    a.time_span = t1 - t0;
+  }
   a.tiles_x_magic = a.tiles_x > 1u ? UINT64_MAX / a.tiles_x + 1u : 0u;
   a.tile_ids = d_tiles;
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)

@@ -128,6 +128,22 @@ def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
         assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
 
 
+def test_pass_with_path_ids_above_2_31(gpu, monkeypatch):
+    """One pass of more than 2^31 paths (monument-4k's passes hold 2^32): path ids past 2^31 must
+    dispense and index correctly.  The same frame split into 2^30-path passes is the reference."""
+    rtw = gpu
+    s = rtw.Scene()
+    cam, bg = s.preset("two-spheres", 1.0, seed=3)
+    s.commit()
+    w = h = 256
+    spp = 32800  # 256 * 256 * 32800 = 2.15e9 paths > 2^31
+    one, st1 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=7).render()
+    monkeypatch.setenv("RTW_PASS_LOG2", "30")
+    split, st2 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=7).render()
+    assert st1["rays"] == st2["rays"] > w * h * spp
+    assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
+
+
 def test_path_kernel_times(gpu):
     rtw = gpu
     s = rtw.Scene()
