@@ -826,7 +826,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   const uint64_t P = a.n_paths;
   uint32_t cnt[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
-  uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
+  // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
+  // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
+  __shared__ uint64_t pool_lds[BLOCK / 64][3];
+  uint64_t* const pool = pool_lds[threadIdx.x >> 6];
+  if (lane == 0) { pool[0] = 0; pool[1] = 0; }
   bool exhausted = false;                // wave-uniform
   bool has = false;
   TraceState ts;
@@ -853,14 +857,14 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t n_need = (uint32_t)__popcll(need);
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      uint64_t pool_next = rfl64(pool[0]), pool_end = rfl64(pool[1]);
       const uint64_t avail = pool_end - pool_next;
       uint64_t nb = P, ne = P;
       if (avail < n_need) {  // refill: one atomic per BATCH paths
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(a.queue, (unsigned long long)BATCH);
-        b = __shfl(b, 0, 64);
-        // wave-uniform: keep the pool bounds in SGPRs (frees VGPRs the allocator otherwise spills)
-        b = rfl64(b);
+        // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
+        // for the other lanes would be one more loop-carried VGPR pair)
+        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)BATCH);
+        const uint64_t b = rfl64(pool[2]);
         if (b < P) {
           nb = b;
           ne = b + BATCH < P ? b + BATCH : P;
@@ -879,8 +883,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
         pool_end = ne;
         if (pool_next > pool_end) pool_next = pool_end;
       }
-      pool_next = rfl64(pool_next);  // uniform by construction; tell the register allocator
-      pool_end = rfl64(pool_end);
+      if (lane == 0) { pool[0] = pool_next; pool[1] = pool_end; }
     }
     if (__ballot(has) == 0) {
       if (exhausted) break;
