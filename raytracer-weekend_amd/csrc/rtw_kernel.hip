@@ -1249,9 +1249,9 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
     // (RTW_REGEN_MIN sweep 1..32): 24 is best for open scenes (jumpy-balls +4.3%, cow +1.6%,
     // monument +1.7% over 1); closed boxes (cornell: 6.6 segments per path, few lanes finish per
-    // iteration) lose with deferral, so they use 4.
+    // iteration) lose with deep deferral: 8 (cornell list variant at 8 waves/SIMD: 29.3k at 1, 29.4k at 4, 29.8k at 8, 28.1k at 24).
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
-    a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 4 : 24)));
+    a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
     const int grid = resident_grid(c, fn, count);
     const uint32_t lds = var.stack;
     a.spill_depth = sc.flat.stack_need > lds ? sc.flat.stack_need - lds : 0;
