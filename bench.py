@@ -3,20 +3,28 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config jumpy-1080p]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+    python bench.py --multi-device N      # one process drives N GPUs through rtw_render_multi
 
 A step = one full frame of the configured workload (default: BASELINE.json configs[1],
 RTOW final random-spheres "jumpy-balls", 1920x1080, 512 spp, 50 bounces) rendered by the
 hot path, with the scene already resident in HBM.  The frame's 8x8 tiles are dealt
-round-robin to the N ranks (one process per GPU); each rank renders its tiles with
-rtw_render_device, then one RCCL all-gather over xGMI brings every rank's packed tiles to
-all ranks and rank 0 unpacks the framebuffer and copies it to the host.  Total work is
-fixed as N grows ("scaling": "strong").  value = rays of the frame (world.hit queries,
+round-robin to the N ranks (one process per GPU, rtw_tile_partition); each rank renders its
+tiles with rtw_render_device, then one RCCL all-gather over xGMI brings every rank's packed
+tiles to all ranks and rank 0 unpacks the framebuffer and copies it to the host.  Total work
+is fixed as N grows ("scaling": "strong").  value = rays of the frame (world.hit queries,
 lib.rs:102, counted exactly by the kernel) / max-over-ranks step time.
 
-Also reported: `roofline` for the render kernel (algorithmic bytes per launch from the
-traversal counters / its average HIP-event duration, vs 8 TB/s HBM) and `cpu_baseline`
-(the oracle — the reference algorithm restated in C, flat-list closest hit — timed on the
-host cores over a bounded sample of the same frame, rank 0 at N=1 only).
+`roofline`: the path kernel is bound by VALU issue (SQ counters), so the
+roofline is FP32 VALU: algorithmic flops per launch (SURVEY.md §8d / BASELINE.md: 21 per box
+tested, 23 per sphere test (+12 moving), 6 per rect, 51 per triangle, + the shading and camera
+constants below) / the kernel's average HIP-event duration, vs the 157.3 TFLOP/s FP32 vector
+peak.  Reported beside it: the measured HBM fraction (rocprofv3 PMC bytes per launch / duration /
+8 TB/s), the SQ-counter VALU lane-capacity figure (VALU busy x lane utilisation) and the
+cache-level algorithmic bytes.  scripts/roofline.py recomputes all of them from profiles/.
+
+`cpu_baseline` is the oracle (the reference algorithm restated in C, flat-list closest hit,
+recursive sample_ray; -O3) on every host core of the box, best of 3 over a bounded row sample
+of the same frame, rank 0 at N=1 only.
 """
 from __future__ import annotations
 
@@ -44,12 +52,17 @@ CONFIGS = {
 }
 SCENE_SEED = 42      # replaces thread_rng() in scenes.rs
 RENDER_SEED = 2024
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# BASELINE.md roofline definition: algorithmic bytes per ray
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
+# FP32 flop model (BASELINE.md roofline; DESIGN.md §5 derives each constant)
+FLOP_BOX = 21              # aabb.rs:23-48: per axis 1 div + 2 sub + 2 mul + min + max
+FLOP_PRIM = [23, 35, 6, 6, 6, 51]  # sphere (spherical.rs:26-44), moving (+12, :117-123), rect xy/xz/yz, triangle
+FLOP_SEGMENT = 60          # hit record + scatter + throughput per world.hit query
+FLOP_PATH = 50             # Camera::get_ray + pixel u, v per path (camera.rs:66-74, lib.rs:84-85)
+# cache-level algorithmic bytes (the round-1 figure; operands come from L1/L2, not HBM)
 RAY_STATE_B = 64
-NODE_BOX_B = 32            # per box tested
-BOXES_PER_NODE = 4         # one DevNode4 fetch tests 4 child boxes (BVH4)
-PRIM_B = [16, 36, 20, 20, 20, 36]  # sphere, moving sphere, rect xy/xz/yz, triangle
+NODE_BOX_B = 32
+PRIM_B = [16, 36, 20, 20, 20, 36]
 
 
 def _load(name, path, pkg_dir=None):
@@ -63,33 +76,13 @@ def _load(name, path, pkg_dir=None):
     return mod
 
 
-def cpu_baseline(rtw, scene, cam, bg, w, h, spp, budget_s: float, threads: int) -> dict:
-    """The oracle (reference algorithm: flat-list closest hit, recursive sample_ray) on a
-    bounded, evenly strided sample of the frame's rows, at the frame's spp."""
-    orc = _load("rtw_oracle_py", ROOT / "oracle" / "oracle.py")
-    o = orc.OracleScene(scene.dump(), scene.images())
-    ocam = orc.camera_from_fields(cam.as_dict())
-    rays = 0
-    rows_done = 0
-    elapsed = 0.0
-    spp_s = max(1, min(spp, 8))
-    order = list(range(0, h, 37)) + [j for j in range(h) if j % 37]  # strided first
-    k = 0
-    chunk = max(1, threads)
-    while elapsed < budget_s and k < len(order):
-        rows = order[k:k + chunk]
-        k += chunk
-        t0 = time.perf_counter()
-        _, r = o.render(ocam, bg, w, h, spp_s, seed=RENDER_SEED, integrator=orc.RECURSIVE,
-                        bvh_mode=orc.BVH_REFERENCE, threads=threads, rows=rows)
-        elapsed += time.perf_counter() - t0
-        rays += r
-        rows_done += len(rows)
-        chunk = min(chunk * 2, 4 * threads)
-    return {"value": round(rays / elapsed / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{rows_done} of {h} rows x {w} px x {spp_s} spp of the same frame "
-                      f"({rays} rays in {elapsed:.1f} s, oracle/rtw_oracle.c, {threads} threads, "
-                      f"CPU {cpu_model()})"}
+def cpu_quota() -> float | None:
+    """CPUs this process may use per the cgroup (cpu.max), None if unlimited / unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model() -> str:
@@ -102,6 +95,71 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_baseline(scene, cam, bg, w, h, spp, budget_s: float) -> dict:
+    """The oracle (reference algorithm: flat-list closest hit / the reference BvhNode tree,
+    recursive sample_ray) on every host core, best of 3 over the same evenly strided row sample
+    of the frame (at min(spp, 8) samples per pixel)."""
+    orc = _load("rtw_oracle_py", ROOT / "oracle" / "oracle.py")
+    o = orc.OracleScene(scene.dump(), scene.images())
+    ocam = orc.camera_from_fields(cam.as_dict())
+    threads = min(256, os.cpu_count() or 1)  # oracle_render's thread cap
+    spp_s = max(1, min(spp, 8))
+    order = list(range(0, h, 37)) + [j for j in range(h) if j % 37]  # strided first
+
+    def run(rows):
+        t0 = time.perf_counter()
+        _, r = o.render(ocam, bg, w, h, spp_s, seed=RENDER_SEED, integrator=orc.RECURSIVE,
+                        bvh_mode=orc.BVH_REFERENCE, threads=threads, rows=rows)
+        return time.perf_counter() - t0, r
+
+    probe = order[:max(1, threads)]
+    dt, _ = run(probe)
+    n = int(min(len(order), max(len(probe), len(probe) * (budget_s / 3.0) / max(dt, 1e-3))))
+    rows = order[:n]
+    times, rays = [], 0
+    for _ in range(3):
+        dt, rays = run(rows)
+        times.append(dt)
+    best = min(times)
+    return {"value": round(rays / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cpu_quota_cores": cpu_quota(), "nproc": os.cpu_count(),
+            "label": f"CPU restatement, {threads} threads; baseline only",
+            "sample": f"{len(rows)} of {h} rows x {w} px x {spp_s} spp of the same frame, best of 3 "
+                      f"({rays} rays in {best:.2f} s; runs {', '.join(f'{t:.2f}' for t in times)} s), "
+                      f"oracle/rtw_oracle.c -O3, {threads} threads, CPU {cpu_model()}"}
+
+
+def flops_model(counts: dict) -> float:
+    """Algorithmic FP32 flops of the counted work."""
+    return (FLOP_BOX * counts["boxes"] + float(np.dot(counts["prims"], FLOP_PRIM))
+            + FLOP_SEGMENT * counts["rays"] + FLOP_PATH * counts["paths"])
+
+
+def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: int, traffic, issue) -> dict:
+    """The path kernel's roofline figures for one launch (this rank's share of the frame)."""
+    flops = flops_model(counts) / world / launches
+    tflops = flops / (kernel_ms_per_launch * 1e-3) / 1e12
+    alg_bytes = (RAY_STATE_B * counts["rays"] + NODE_BOX_B * counts["boxes"]
+                 + float(np.dot(counts["prims"], PRIM_B))) / world / launches
+    out = {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
+           "flops_per_launch": round(flops), "kernel_ms_per_launch": round(kernel_ms_per_launch, 3),
+           "flops_per_ray": round(flops_model(counts) / max(1, counts["rays"]), 1),
+           "hbm": None, "valu_lane": None,
+           "cache_level": {"alg_bytes_per_launch": round(alg_bytes),
+                           "GBps": round(alg_bytes / (kernel_ms_per_launch * 1e-3) / 1e9, 1),
+                           "note": "node/prim operands are L1/L2 hits; not an HBM figure"}}
+    if traffic:
+        gbs = traffic / (kernel_ms_per_launch * 1e-3) / 1e9
+        out["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_launch": traffic}
+    if issue and issue.get("valu_busy") and issue.get("valu_lane_util"):
+        out["valu_lane"] = {"valu_busy": issue["valu_busy"], "lane_util": issue["valu_lane_util"],
+                            "frac": round(issue["valu_busy"] * issue["valu_lane_util"], 4),
+                            "source": issue.get("source")}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,13 +168,16 @@ def main() -> int:
     ap.add_argument("--config", default="jumpy-1080p", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override spp (changes the workload!)")
     ap.add_argument("--launches", type=int, default=0, help="kernel launches per frame (0 = auto)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work (3 runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default="", help="PMC HBM bytes per launch (from profiles/)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path on one GPU")
     ap.add_argument("--check-image", action="store_true",
                     help="rank 0 checks the gathered frame bit-for-bit against a single-device render")
+    ap.add_argument("--multi-device", type=int, default=0,
+                    help="N > 0: one process renders each frame on N GPUs through rtw_render_multi "
+                         "(C-ABI, RCCL send/recv gather to device 0, frame copied to the host)")
     args = ap.parse_args()
 
     import torch
@@ -143,19 +204,20 @@ def main() -> int:
         spp = args.spp
     scene = rtw.Scene()
     cam, bg = scene.preset(scene_name, rtw.camera_aspect(w, h), seed=SCENE_SEED)
-    scene.commit(device=dev)
+    multi = args.multi_device if world == 1 else 0
+    scene.commit(device=-1 if multi else dev)
     rt = rtw.Raytracer(scene, cam, bg, w, h, spp, seed=RENDER_SEED)
 
     # tiles of this rank (round-robin interleave balances sky rows against ground rows)
     nt = rtw.n_tiles(w, h)
-    per_rank = (nt + world - 1) // world
-    ids = torch.arange(rank, nt, world, dtype=torch.int32, device=dev)
-    n_mine = int(ids.numel())
+    pad_ids, n_mine = rtw.tile_partition(w, h, world, rank)
+    per_rank = len(pad_ids)
+    ids = torch.tensor(pad_ids.astype(np.int32), dtype=torch.int32, device=dev)
     packed = torch.zeros((per_rank, 64, 3), dtype=torch.float32, device=dev)
     gathered = torch.zeros((world * per_rank, 64, 3), dtype=torch.float32, device=dev) if world > 1 else None
     if world > 1:  # rank-major tile ids of the gathered buffer, padded with nt (= skipped)
-        pad = [list(range(r, nt, world)) + [nt] * (per_rank - len(range(r, nt, world))) for r in range(world)]
-        all_ids = torch.tensor(np.array(pad, np.int32).reshape(-1), dtype=torch.int32, device=dev)
+        lay = np.concatenate([rtw.tile_partition(w, h, world, r)[0] for r in range(world)]).astype(np.int32)
+        all_ids = torch.tensor(lay, dtype=torch.int32, device=dev)
     else:
         all_ids = ids
     image = torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
@@ -164,18 +226,18 @@ def main() -> int:
 
     launches = args.launches or 1  # persistent path kernel: one launch drains the whole frame
     bounds = np.linspace(0, n_mine, launches + 1).astype(int)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
 
-    def render_frame(record: bool):
+    def render_frame():
+        if multi:
+            rt.render_multi(multi)  # blocking: renders, gathers over RCCL, copies the frame to the host
+            return
         for k in range(launches):
             a, b = int(bounds[k]), int(bounds[k + 1])
-            if record:
-                ev[k][0].record(stream)
             rt.render_device(packed[a:].data_ptr(), dev, ids[a:].data_ptr(), b - a, stream.cuda_stream)
-            if record:
-                ev[k][1].record(stream)
 
     def frame_end():
+        if multi:
+            return
         if world > 1 and args.backend == "gloo":  # CPU rehearsal: gather through host memory
             g = torch.zeros(gathered.shape, dtype=torch.float32)
             dist.all_gather_into_tensor(g, packed.cpu())
@@ -197,36 +259,43 @@ def main() -> int:
     # exact ray count + traversal counters of this rank's share (untimed, same seed => same work)
     st = rt.render_device(packed.data_ptr(), dev, ids.data_ptr(), n_mine, stream.cuda_stream,
                           flags=rtw.FLAG_COUNT_TRAVERSAL, want_stats=True)
-    counts = torch.tensor([st["rays"], st["node_visits"]] + st["prim_tests_by_type"], dtype=torch.float64,
-                          device=dev)
+    counts = torch.tensor([st["rays"], st["node_visits"], st["boxes_tested"], n_mine * 64 * spp]
+                          + st["prim_tests_by_type"], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(counts)
     counts = counts.cpu().numpy()
     frame_rays = int(counts[0])
+    cnt = {"rays": counts[0], "node4": counts[1], "boxes": counts[2], "paths": min(counts[3], w * h * spp),
+           "prims": counts[4:10]}
 
     for _ in range(args.warmup):
-        render_frame(False)
+        render_frame()
         frame_end()
     if args.check_image:  # the gathered frame must equal a single-device render, bit for bit
-        render_frame(False)
+        render_frame()
         frame_end()
         torch.cuda.synchronize()
         if rank == 0:
             ref = torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
             rt.render_device(ref.data_ptr(), dev, 0, 0, stream.cuda_stream)
             torch.cuda.synchronize()
-            same = bool(torch.equal(ref.view(torch.int32), image.view(torch.int32)))
-            print(json.dumps({"check_image": same, "world": world}), flush=True)
+            if multi:
+                got, _ = rt.render_multi(multi)
+                same = bool(np.array_equal(ref.cpu().numpy().view(np.uint32), got.view(np.uint32)))
+            else:
+                same = bool(torch.equal(ref.view(torch.int32), image.view(torch.int32)))
+            print(json.dumps({"check_image": same, "world": world, "multi_device": multi}), flush=True)
             if not same:
                 raise SystemExit("gathered frame differs from the single-device render")
     torch.cuda.synchronize()
-    scene.path_kernel_times(dev)  # forget the untimed launches
+    for d in (range(multi) if multi else [dev]):
+        scene.path_kernel_times(d)  # forget the untimed launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        render_frame(True)
+        render_frame()
         frame_end()
     torch.cuda.synchronize()
     if world > 1:
@@ -237,10 +306,9 @@ def main() -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    call_ms = float(sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(launches)))  # last step: path + reduce
-    # path_kernel alone: the library's HIP events around each launch on this stream, all K steps
-    # (a render call splits a frame larger than MAX_PASS_PATHS into several passes, one launch each)
-    pk = scene.path_kernel_times(dev)  # the last min(64, K * launches * passes) launches
+    # path_kernel alone: the library's HIP events around each launch on the launch stream, all K
+    # steps (a render call splits a frame larger than 2^32 paths into several passes, one launch each)
+    pk = scene.path_kernel_times(0 if multi else dev)
     if not pk or len(pk) >= 64 or len(pk) % (args.steps * launches):
         raise SystemExit(f"path-kernel timings: got {len(pk)} for {args.steps} steps x {launches} calls "
                          "(ring of 64 overflowed or launches missing; lower --steps)")
@@ -248,36 +316,42 @@ def main() -> int:
     frame_kernel_ms = float(sum(pk)) / args.steps
 
     value = frame_rays * args.steps / dt / 1e6
-    # roofline of the render kernel (this rank): algorithmic bytes per launch / avg launch time
-    rays_r = counts[0]
-    nodes_r = counts[1]
-    prim_bytes = float(np.dot(counts[2:8], PRIM_B))
-    alg_bytes_frame = RAY_STATE_B * rays_r + BOXES_PER_NODE * NODE_BOX_B * nodes_r + prim_bytes
-    alg_bytes_rank = alg_bytes_frame / world
-    achieved = alg_bytes_rank / (frame_kernel_ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes; scripts/gpu_profile.sh + scripts/prof_summary.py), if any
     traffic, traffic_src = None, None
     tj = Path(args.traffic_json) if args.traffic_json else ROOT / "profiles" / f"pmc_{args.config}.json"
-    if tj.exists() and not args.spp:
+    if tj.exists() and not args.spp and not multi:
         d = json.loads(tj.read_text())
         if d.get("launches_per_frame", 1) == launches and d.get("world", 1) == world:
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(ROOT))
-    # what does bound it: SQ counters of the same config (scripts/gpu_counters.sh + valu_summary.py)
+    # what bounds it: SQ counters of the same config (scripts/gpu_counters.sh + valu_summary.py)
     issue = None
     vj = ROOT / "profiles" / f"valu_{args.config}.json"
     if vj.exists() and not args.spp:
         d = json.loads(vj.read_text())
         issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit")}
         issue["source"] = str(vj.relative_to(ROOT))
+    n_launch = launches * passes
+    # per launch of this rank (multi-device: device 0's launches, its 1/N share of the frame)
+    roof = roofline(cnt, frame_kernel_ms / n_launch, n_launch, multi or world, traffic, issue)
 
     out = None
     if rank == 0:
+        n_dev = multi or world
+        roof.update({"traffic_source": traffic_src, "issue_counters": issue, "kernel": "path_kernel",
+                     "kernel_ms_per_frame": round(frame_kernel_ms, 3), "kernel_launches_per_frame": n_launch,
+                     "node_fetches_per_ray": round(cnt["node4"] / max(1, cnt["rays"]), 3),
+                     "boxes_per_ray": round(cnt["boxes"] / max(1, cnt["rays"]), 3),
+                     "prim_tests_per_ray": round(float(cnt["prims"].sum()) / max(1, cnt["rays"]), 3),
+                     "counts": {"rays": int(cnt["rays"]), "paths": int(cnt["paths"]), "node4": int(cnt["node4"]),
+                                "boxes": int(cnt["boxes"]), "prims_by_type": [int(x) for x in cnt["prims"]]},
+                     "simd_util_rank0": {k: (round(v, 3) if v else v) for k, v in st["simd_util"].items()},
+                     "phase_share_rank0": {k: (round(v, 3) if v else v) for k, v in st["phase_share"].items()}})
         out = {
             "metric": "Mrays/sec at 1920x1080, 512 spp, 50 bounces; 1/2/4/8-GPU scaling",
             "value": round(value, 2),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": n_dev,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -286,26 +360,16 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded scene generator, scenes.rs restated; seed %d)" % SCENE_SEED,
-            "config": {"workload": cfg_text, "backend": args.backend if world > 1 else None, "scene": scene_name, "width": w, "height": h, "spp": spp,
-                       "max_depth": 50, "rays_per_frame": frame_rays, "paths_per_frame": w * h * spp,
-                       "tiles": nt, "launches_per_frame": launches, "parallelism": f"tiles{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": traffic_src, "issue_counters": issue, "kernel": "path_kernel",
-                         "kernel_ms_per_frame": round(frame_kernel_ms, 3),
-                         "kernel_launches_per_frame": launches * passes,
-                         "alg_bytes_per_launch": round(alg_bytes_rank / (launches * passes)),
-                         "render_call_ms_last_frame": round(call_ms, 3),
-                         "alg_bytes_per_ray": round(alg_bytes_frame / max(1, frame_rays), 2),
-                         "node_fetches_per_ray": round(nodes_r / max(1, rays_r), 3),
-                         "prim_tests_per_ray": round(float(counts[2:8].sum()) / max(1, rays_r), 3),
-                         "simd_util_rank0": {k: (round(v, 3) if v else v) for k, v in st["simd_util"].items()},
-                         "phase_share_rank0": {k: (round(v, 3) if v else v) for k, v in st["phase_share"].items()}},
+            "config": {"workload": cfg_text, "backend": args.backend if world > 1 else ("rccl" if multi else None),
+                       "scene": scene_name, "width": w, "height": h, "spp": spp, "max_depth": 50,
+                       "rays_per_frame": frame_rays, "paths_per_frame": w * h * spp, "tiles": nt,
+                       "launches_per_frame": launches,
+                       "parallelism": f"tiles{n_dev}" + ("-single-process" if multi else "")},
+            "roofline": roof,
             "paths_per_sec": round(w * h * spp * args.steps / dt, 1),
         }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(rtw, scene, cam, bg, w, h, spp, args.cpu_budget, threads)
+        if n_dev == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, cam, bg, w, h, spp, args.cpu_budget)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

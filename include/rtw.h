@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 3
+#define RTW_ABI_VERSION 4
 
 enum {
   RTW_OK = 0,
@@ -65,6 +65,11 @@ typedef struct {
   /* RTW_FLAG_COUNT_TRAVERSAL: wave-cycles (s_memtime) spent in path regeneration, closest-hit
    * traversal and shading, and in the whole path kernel, summed over waves */
   uint64_t phase_cycles[4];
+  /* RTW_FLAG_COUNT_TRAVERSAL: child boxes slab-tested (the non-empty slots of the visited 4-wide
+   * nodes), and the wave-cycles of shading spent in random_in_unit_sphere (part of phase_cycles[2]'s
+   * shading time, counted apart from it) */
+  uint64_t boxes_tested;
+  uint64_t sample_cycles;
 } rtw_stats;
 
 enum { RTW_FLAG_COUNT_TRAVERSAL = 1 };
@@ -210,12 +215,36 @@ int rtw_progress_decode(const uint8_t* frame, size_t len, rtw_progress_msg* msg)
  * tile id = ty * ceil(w/8) + tx.  If d_tile_ids == NULL all tiles are rendered and d_out is a
  * full w*h*3 image in reference order; otherwise d_tile_ids is a DEVICE array of n_tiles ids
  * and d_out is packed [n_tiles][64][3] (pixels outside the image, and ids beyond the last tile,
- * are left untouched).  `stream` is a hipStream_t (NULL = default).  The call only enqueues
- * (graph-capturable) unless stats != NULL, in which case it synchronises and fills stats. */
+ * are left untouched).  `stream` is a hipStream_t (NULL = default).  The call only enqueues unless
+ * stats != NULL, in which case it synchronises and fills stats.  Each (scene, device) pair owns one
+ * path queue and one sample buffer: renders of a scene on one device must be serialised on one
+ * stream (two renders in flight on different streams would share them).  The first render of a
+ * given size allocates the sample buffer (hipMalloc: not stream-capturable); later renders of the
+ * same or a smaller size only enqueue. */
 int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float background[3],
                       uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
                       const uint32_t* d_tile_ids, uint32_t n_tiles, float* d_out, void* stream,
                       uint32_t flags, rtw_stats* stats);
+
+/* Raytracer::new(..).render().collect() (lib.rs:40-95) over n_gpus devices of this node, driven from
+ * the calling host thread (the reference's Rayon pixel parallelism, lib.rs:57-76, becomes tiles
+ * across GPUs).  Tile k goes to device k mod n (rtw_tile_partition); each device renders its tiles
+ * on its own stream with its own copy of the scene (commit with device = -1 first); one RCCL gather
+ * over xGMI (grouped ncclSend to device 0 / ncclRecv on device 0; librccl.so.1 is opened on first
+ * use) brings the tiles to device 0, which assembles the frame and copies it into out_rgb_sum in the
+ * same layout as rtw_render.  n_gpus <= 0 = every visible device.  The frame is bit-identical to
+ * rtw_render's for every n_gpus (per-pixel random streams).  stats->rays sums the devices,
+ * stats->kernel_ms is the slowest device's.  Blocking. */
+int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const float background[3], uint32_t w,
+                     uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, float* out_rgb_sum,
+                     rtw_stats* stats);
+
+/* The frame partition rtw_render_multi (and bench.py's one-process-per-GPU path) uses: the 8x8 tiles
+ * of a w x h frame dealt round-robin to n_parts parts; part p gets tiles p, p + n, p + 2n, ...
+ * Writes min(cap, ceil(nt / n)) ids (the part's tiles, then padding ids equal to nt, which
+ * rtw_unpack_tiles_device skips) and the part's real tile count to *n_ids.  Host only. */
+int rtw_tile_partition(uint32_t w, uint32_t h, uint32_t n_parts, uint32_t part, uint32_t* ids, uint32_t cap,
+                       uint32_t* n_ids);
 
 /* Scatter packed tiles (as written by rtw_render_device) into a full device image. */
 int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* d_tile_ids,

@@ -52,7 +52,7 @@ class rtw_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("kernel_ms", C.c_double),
                 ("total_ms", C.c_double), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("prim_tests_by_type", C.c_uint64 * 6), ("simd", C.c_uint64 * 6),
-                ("phase_cycles", C.c_uint64 * 4)]
+                ("phase_cycles", C.c_uint64 * 4), ("boxes_tested", C.c_uint64), ("sample_cycles", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {"rays": int(self.rays), "paths": int(self.paths), "kernel_ms": float(self.kernel_ms),
@@ -61,8 +61,10 @@ class rtw_stats(C.Structure):
                 "prim_tests_by_type": [int(x) for x in self.prim_tests_by_type],
                 "simd_util": {k: (self.simd[2 * q + 1] / (64.0 * self.simd[2 * q]) if self.simd[2 * q] else None)
                               for q, k in enumerate(("node_loop", "prim_tests", "segments"))},
-                "phase_share": {k: (self.phase_cycles[q] / self.phase_cycles[3] if self.phase_cycles[3] else None)
-                                for q, k in enumerate(("regen", "trace", "shade"))}}
+                "boxes_tested": int(self.boxes_tested),
+                "phase_share": dict({k: (self.phase_cycles[q] / self.phase_cycles[3] if self.phase_cycles[3] else None)
+                                     for q, k in enumerate(("regen", "trace", "shade"))},
+                                    sample=(self.sample_cycles / self.phase_cycles[3] if self.phase_cycles[3] else None))}
 
 
 class rtw_pixel(C.Structure):  # lib.rs:120-126 Pixel
@@ -119,6 +121,9 @@ _SIGS = {
                                     C.c_uint32, C.c_uint32, C.c_uint64, _U32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
     "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
+    "rtw_render_multi": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, C.c_uint32, C.c_uint64, _F, C.POINTER(rtw_stats)]),
+    "rtw_tile_partition": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _U32, C.c_uint32, _U32]),
     "rtw_render_stream": (C.c_int, [C.c_void_p, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_uint64, C.c_uint32, PIXEL_SINK, C.c_void_p,
                                     C.POINTER(rtw_stats)]),
@@ -141,7 +146,7 @@ EXPORTED_SYMBOLS = tuple(_SIGS)
 _lib = None
 
 
-ABI_VERSION = 3  # include/rtw.h RTW_ABI_VERSION
+ABI_VERSION = 4  # include/rtw.h RTW_ABI_VERSION
 
 
 def lib() -> C.CDLL:
@@ -412,6 +417,15 @@ class Raytracer:
                                 self.max_depth, self.seed, out.ctypes.data_as(_F), C.byref(st)))
         return out, st.as_dict()
 
+    def render_multi(self, n_gpus: int = 0):
+        """The same frame over n_gpus devices from this thread (rtw_render_multi: interleaved tiles,
+        one RCCL gather to device 0); n_gpus <= 0 = every visible device.  -> (sums, stats)."""
+        out = np.empty((self.h, self.w, 3), np.float32)
+        st = rtw_stats()
+        _check(lib().rtw_render_multi(self.scene._p, int(n_gpus), C.byref(self.cam.c), _fp(self.bg), self.w, self.h,
+                                      self.spp, self.max_depth, self.seed, out.ctypes.data_as(_F), C.byref(st)))
+        return out, st.as_dict()
+
     def render_stream(self, on_pixels, band_rows: int = 64):
         """Raytracer::render() as a progressive Pixel stream (lib.rs:50-76): on_pixels(array of
         PIXEL_DTYPE records) per finished band, in emission order (row j = h-1 .. 0).  -> stats."""
@@ -502,6 +516,16 @@ def diag_libm(fn: int, a, b=None) -> np.ndarray:
     out = np.empty_like(a)
     _check(lib().rtw_diag_libm(fn, len(a), _fp(a), _fp(bb) if bb is not None else None, _fp(out)))
     return out
+
+
+def tile_partition(w: int, h: int, n_parts: int, part: int):
+    """rtw_tile_partition -> (padded ids of the part [ceil(nt / n_parts)], number of real ids)."""
+    nt = n_tiles(w, h)
+    per = (nt + n_parts - 1) // n_parts if n_parts > 0 else 0
+    ids = np.zeros(max(1, per), np.uint32)
+    n = C.c_uint32()
+    _check(lib().rtw_tile_partition(w, h, n_parts, part, _up(ids), per, C.byref(n)))
+    return ids[:per], int(n.value)
 
 
 def n_tiles(w: int, h: int) -> int:

@@ -95,6 +95,22 @@ struct alignas(16) DevPerlin {
   uint8_t perm[3][256];
 };
 
+// Per leaf primitive (same index as prims[]): its material and, for the common textures, the texture
+// values themselves, so that shading needs ONE load once the closest hit is known instead of the
+// prim -> material -> texture -> checker-child chain of dependent loads.  32 B.
+enum ShadeMode : uint32_t {
+  SM_GENERIC = 0,  // read mats[prim.mat] / texs[] (image, noise, uv-debug, nested checkers)
+  SM_SOLID = 1,    // SolidColor: a = colour (texture.rs:56-60); Metal: a = albedo
+  SM_CHECKER = 2,  // Checker(SolidColor odd, SolidColor even, freq): a = odd, b = even (texture.rs:69-81)
+};
+struct alignas(16) DevShade {
+  uint32_t kind;  // bits 0..7 MatType, bits 8..11 ShadeMode, bit 12 the material reads uv
+  float param;    // metal fuzz | dielectric ir | checker frequency (Lambertian / light / isotropic)
+  float a[3];
+  float b[3];
+};
+static_assert(sizeof(DevShade) == 32, "DevShade must be 32 B");
+
 // Scene features: the path kernel is instantiated per feature set so a scene only pays (in code
 // size and register pressure) for the primitive / wrapper / material / texture kinds it uses.
 enum Feature : uint32_t {
@@ -137,6 +153,7 @@ struct DevScene {
   const DevTex* texs;
   const uint8_t* texels;
   const DevPerlin* perlins;
+  const DevShade* shade;
   uint32_t n_nodes, n_prims, n_always, n_insts;
 };
 
@@ -163,7 +180,7 @@ struct RenderArgs {
   uint64_t n_paths;           // paths in this pass = slots * 64 * spp
   float* sbuf;                // ordered sample buffer: n_paths x (r, g, b) floats, path-major
   float* out;
-  unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
+  unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type, [30] error flag
   unsigned long long* queue;     // path-id dispenser of this pass
   int32_t* spill;                // traversal stack entries beyond the LDS stack: [depth][lane]
   uint32_t spill_depth;          // entries per lane (0 = the LDS stack covers the tree's bound)

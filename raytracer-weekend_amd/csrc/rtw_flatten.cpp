@@ -580,6 +580,34 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // shading records (one per prim, same order)
+  for (const DevPrim& p : f.prims) {
+    const DevMat& m = f.mats[p.mat];
+    DevShade d;
+    memset(&d, 0, sizeof d);
+    uint32_t mode = SM_GENERIC;
+    if (m.type == MT_METAL) {
+      mode = SM_SOLID;
+      memcpy(d.a, m.albedo, sizeof d.a);
+      d.param = m.param;
+    } else if (m.type == MT_DIELECTRIC) {
+      mode = SM_SOLID;  // attenuation (1, 1, 1), no texture
+      d.param = m.param;
+    } else {  // Lambertian, DiffuseLight, Isotropic: a texture
+      const DevTex& t = f.texs[m.tex];
+      if (t.type == TT_SOLID) {
+        mode = SM_SOLID;
+        memcpy(d.a, t.c, sizeof d.a);
+      } else if (t.type == TT_CHECKER && f.texs[t.odd].type == TT_SOLID && f.texs[t.even].type == TT_SOLID) {
+        mode = SM_CHECKER;
+        memcpy(d.a, f.texs[t.odd].c, sizeof d.a);
+        memcpy(d.b, f.texs[t.even].c, sizeof d.b);
+        d.param = t.freq;
+      }
+    }
+    d.kind = m.type | (mode << 8) | (m.needs_uv ? 1u << 12 : 0u);
+    f.shade.push_back(d);
+  }
   // 4-wide tree for the kernel
   if (!f.nodes.empty()) {
     if (rest.size() >= (1u << 28)) return fail(RTW_EINVAL, "too many BVH primitives for leaf words");

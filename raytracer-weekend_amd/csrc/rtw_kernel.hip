@@ -26,6 +26,7 @@
 #include <chrono>
 
 #include "../../include/rtw.h"
+#include "rtw_checker.h"
 #include "rtw_scene.hpp"
 
 namespace rtw {
@@ -467,7 +468,8 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // every lane of the wave holds a leaf or has run dry; phase 2 tests all parked leaves together.
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
-                          uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint64_t seg) {
+                          uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint64_t seg,
+                          unsigned long long* err) {
   auto safe_inv = [](float d) {
     float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
     return __builtin_amdgcn_rcpf(dd);
@@ -479,9 +481,13 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
   const char* const NB = reinterpret_cast<const char*>(S.nodes);
-  // every wave must drain: a corrupt tree (cycle) ends the walk instead of hanging the GPU
-  for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
-    for (uint32_t g2 = 0; g2 < (1u << 20); ++g2) {
+  // every wave must drain: a corrupt tree (a cycle) ends the walk instead of hanging the GPU, and
+  // raises the launch's error flag (counters[30]), which the host turns into RTW_EINVAL
+  constexpr uint32_t GUARD = 1u << 20;
+  uint32_t guard = 0;
+  for (; guard < GUARD; ++guard) {
+    uint32_t g2 = 0;
+    for (; g2 < GUARD; ++g2) {
       {  // refill from the stack: an internal node, or a parked leaf if the slot is free
         const bool can = ts.node < 0 && ts.sp > 0;
         int32_t top = 0;
@@ -506,7 +512,11 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
         const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
         const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + 96u));
-        if (COUNT) { cnt[0]++; simd_tick(cnt, 8, 9); }
+        if (COUNT) {
+          cnt[0]++;
+          simd_tick(cnt, 8, 9);
+          cnt[14] += (cw.x != 0) + (cw.y != 0) + (cw.z != 0) + (cw.w != 0);  // child word 0 = empty slot
+        }
         const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
         float tn[4];
         bool hit[4];
@@ -558,6 +568,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         ts.node = next;
       }
     }
+    if (g2 == GUARD) break;
     if (ts.pend != 0) {  // phase 2
       const uint32_t v = ~(uint32_t)ts.pend;
       const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
@@ -565,8 +576,12 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       ts.pend = 0;
     }
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
-    if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) break;
+    if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) return;
   }
+  *err = 1ull;  // a guard tripped: end this traversal (miss) and report
+  ts.node = -1;
+  ts.sp = 0;
+  ts.pend = 0;
 }
 
 // ---- hit record of the winner (hittable/mod.rs:32-48 at every level)
@@ -584,7 +599,7 @@ __device__ __forceinline__ void sphere_uv(V3 p, float& u, float& v) {  // spheri
 }
 
 template <uint32_t FEAT>
-__device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
+__device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint32_t shade_kind) {
   const DevPrim P = S.prims[b.prim];
   const uint32_t type = P.type_inst & 0xffu, inst = P.type_inst >> 8;
   const DevInst* I = S.insts + inst;
@@ -600,7 +615,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
     V3 c = type == PT_SPHERE ? ld3(P.q0) : center_at(P.q0, P.q1, lr.time);
     float rad = type == PT_SPHERE ? P.q0[3] : P.q2[0];
     outward = divs(sub(h.p, c), rad);
-    if ((FEAT & F_UV) && S.mats[P.mat].needs_uv) sphere_uv(outward, h.u, h.v);
+    if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
                          P.q1[2], P.q1[3], P.q2[0], P.q2[1], P.q2[2], P.q2[3]};
@@ -649,22 +664,50 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b) {
   return h;
 }
 
-// Checker::value's decision (texture.rs:69-81) is `sinf(fx) * sinf(fy) * sinf(fz) < 0`.  Only the
-// signs matter when no factor is zero and the product cannot underflow, and sign(sin x) is the
-// parity of floor(x / pi).  oracle/tools/sin_sign_check.c verifies exhaustively that for every
-// float 2^-12 <= |x| < 65536 the double-precision parity equals the sign of libm's sinf and
-// |sinf x| >= 8.4e-9 (so the product of three stays normal): identical decisions, 3 double
-// multiply+floor instead of 3 sinf.  Outside that range the literal expression is evaluated.
+// Checker::value's decision (texture.rs:69-81) is `sinf(fx) * sinf(fy) * sinf(fz) < 0` with glibc's
+// sinf.  oracle/tools/sin_sign_check.cpp proves over EVERY finite float (tests/test_checker_proof.py):
+// sign(sinf x) = parity of floor(x / pi), by the double-precision product for 2^-12 <= |x| < 65536
+// and by the exact integer reduction rtw::pi_parity for |x| >= 65536; sinf x == x for |x| < 2^-12;
+// |sinf x| >= 3.2e-9 for |x| >= 2^-12 (no product of three such factors underflows).  So the
+// decision is the XOR of the factors' signs, except that NaN / inf / 0 factors give "even", and a
+// product with tiny factors below 2^-120 (some |f x| < ~1e-20) is evaluated literally with the
+// correctly rounded dev_sinf (glibc's sinf is <= 1 ulp off: that corner alone is not pinned).
+__device__ __forceinline__ bool checker_odd_slow(float fx, float fy, float fz) {
+  const float f[3] = {fx, fy, fz};
+  uint32_t neg = 0;
+  double lower = 1.0;  // lower bound of |product|
+  bool tiny = false;
+  for (int k = 0; k < 3; ++k) {
+    const float x = f[k];
+    if (x != x || isinf(x) || x == 0.0f) return false;  // NaN or +-0 product: `< 0` is false
+    const float ax = fabsf(x);
+    if (ax < 0x1p-12f) {
+      neg ^= x < 0.0f ? 1u : 0u;
+      lower *= (double)ax;
+      tiny = true;
+    } else {
+      neg ^= pi_parity(ax) ^ (x < 0.0f ? 1u : 0u);
+      lower *= 3.2e-9;
+    }
+  }
+  if (!tiny || lower >= 0x1p-120) return neg != 0;
+  float p = 1.0f;  // the literal left-to-right product (underflow corner)
+  for (int k = 0; k < 3; ++k) {
+    const float x = f[k], ax = fabsf(x);
+    const float s = ax < 0x1p-12f ? x : (ax < 1048576.0f ? dev_sinf(x) : (((pi_parity(ax) ^ (x < 0.0f)) & 1u) ? -1.0f : 1.0f));
+    p = p * s;
+  }
+  return p < 0.0f;
+}
 __device__ __forceinline__ bool checker_odd(float fx, float fy, float fz) {
   const float ax = fabsf(fx), ay = fabsf(fy), az = fabsf(fz);
   const float lo = 0x1p-12f, hi = 65536.0f;
   if (ax >= lo && ax < hi && ay >= lo && ay < hi && az >= lo && az < hi) {
     const double INV_PI = 0.31830988618379067154;
-    const long long k = (long long)floor((double)fx * INV_PI) + (long long)floor((double)fy * INV_PI) +
-                        (long long)floor((double)fz * INV_PI);
+    const int k = (int)floor((double)fx * INV_PI) + (int)floor((double)fy * INV_PI) + (int)floor((double)fz * INV_PI);
     return (k & 1) != 0;
   }
-  return sinf(fx) * sinf(fy) * sinf(fz) < 0.0f;
+  return checker_odd_slow(fx, fy, fz);
 }
 
 // ---- Perlin noise (perlin.rs:50-122), same operation order as the oracle's perlin_noise
@@ -758,7 +801,7 @@ __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // 
 // lanes finish a path, the wave hands them new ids from a per-wave pool (ballot + mbcnt
 // prefix), refilled from a global counter BATCH ids at a time, so lanes stay busy and the
 // grid drains with a one-path tail.  Each finished path writes L to the ordered sample
-// buffer (SoA planes, 12 B/path in HBM); reduce_kernel then sums each pixel's samples in
+// buffer (path-major RGB, 12 B per path in HBM); reduce_kernel then sums each pixel's samples in
 // sample order — exactly lib.rs:83-87's `pixel_color += sample_ray(..)` sequence.
 constexpr uint32_t BATCH = 256;
 
@@ -824,7 +867,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
   const uint64_t P = a.n_paths;
-  uint32_t cnt[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
   // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
@@ -839,7 +882,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   st.pid = 0;
   st.rng = 0;
   st.depth = 0;
-  uint64_t ph[3] = {0, 0, 0};  // COUNT: wave-cycles in regeneration / traversal / shading
+  uint64_t ph[4] = {0, 0, 0, 0};  // COUNT: wave-cycles in regeneration / traversal / shading / shading's
+                                 // rejection sampling
   const uint64_t t_start = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_mark = t_start;
   auto phase = [&](int k) {
@@ -898,7 +942,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     if (!(FEAT & F_LIST)) {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng);
+      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng,
+                                           a.counters + 30);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -914,22 +959,32 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       L = mul(st.T, bg);
       done = true;
     } else {
-      const Rec h = hit_record<FEAT>(S, st.ray, b);
-      const DevMat& m = S.mats[h.mat];
+      // the prim's shading record is loaded as soon as the winner is known, beside its geometry
+      // (one load instead of the prim -> material -> texture -> checker-child chain)
+      const DevShade sh = S.shade[b.prim];
+      const Rec h = hit_record<FEAT>(S, st.ray, b, sh.kind);
       // One body for every material (material.rs:42-165, light_source.rs:17-24): a wave mixing
       // materials runs the rejection loop, unit() and the texture lookup once instead of once per
       // material branch.  Each material's draws and f32 operations are unchanged.
-      const uint32_t mt = m.type;
+      const uint32_t mt = sh.kind & 0xffu, mode = (sh.kind >> 8) & 0xfu;
       const bool light = (FEAT & F_LIGHT) && mt == MT_LIGHT;
       const bool lam = (FEAT & F_LAMBERT) && mt == MT_LAMBERT;
       const bool met = (FEAT & F_METAL) && mt == MT_METAL;
       const bool iso = (FEAT & F_ISO) && mt == MT_ISOTROPIC;
       V3 rs = mk(0.f, 0.f, 0.f);
+      phase(2);
       if (lam || met || iso) rs = rand_in_unit_sphere(st.rng);  // vec3.rs:101-108
+      phase(3);
       const V3 ud = unit(lam ? rs : st.ray.d);                  // Lambertian: unit(rs); else unit(d_in)
       V3 att = mk(1.f, 1.f, 1.f);                                 // Dielectric: attenuation (1,1,1)
-      if (met) att = ld3(m.albedo);
-      else if (light || lam || iso) att = tex_value<FEAT>(S, m.tex, h.u, h.v, h.p);
+      if (met) {
+        att = ld3(sh.a);
+      } else if (light || lam || iso) {
+        if (mode == SM_SOLID) att = ld3(sh.a);  // SolidColor::value
+        else if ((FEAT & F_CHECKER) && mode == SM_CHECKER)
+          att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a) : ld3(sh.b);
+        else att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
+      }
       if (light) {  // emit, no scatter
         L = mul(st.T, att);
         done = true;
@@ -939,10 +994,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
           dir = add(h.n, ud);
           if (near_zero(dir)) dir = h.n;
         } else if (met) {  // material.rs:78-95
-          dir = add(reflect(ud, h.n), scale(rs, m.param));
+          dir = add(reflect(ud, h.n), scale(rs, sh.param));
           done = !(dot(dir, h.n) > 0.0f);  // absorbed: emitted() is black
         } else if (!iso && (FEAT & F_DIEL)) {  // Dielectric, material.rs:116-142
-          const float ratio = h.front ? 1.0f / m.param : m.param;
+          const float ratio = h.front ? 1.0f / sh.param : sh.param;
           const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
           const float sin_t = sqrtf(1.0f - cos_t * cos_t);
           const bool cannot = (ratio * sin_t) > 1.0f;
@@ -969,8 +1024,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (lane == 0) {
       for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
       atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
+      atomicAdd(a.counters + 20, (unsigned long long)ph[3]);
     }
-    for (int q = 0; q < 14; ++q) {
+    for (int q = 0; q < 15; ++q) {
       unsigned long long c = cnt[q];
       for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
       if (lane == 0 && c) atomicAdd(a.counters + 1 + q, c);
@@ -1047,6 +1103,7 @@ int upload(Scene& s, int device) {
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
+  size_t o_shade = put(blob, f.shade);
   blob.resize((blob.size() + 255) & ~(size_t)255);
   int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
   int prev = 0;
@@ -1069,6 +1126,7 @@ int upload(Scene& s, int device) {
     c.scene.texs = (const DevTex*)(base + o_tex);
     c.scene.texels = (const uint8_t*)(base + o_texel);
     c.scene.perlins = (const DevPerlin*)(base + o_perlin);
+    c.scene.shade = (const DevShade*)(base + o_shade);
     c.scene.n_nodes = (uint32_t)f.nodes4.size();
     c.scene.n_prims = (uint32_t)f.prims.size();
     c.scene.n_always = (uint32_t)f.always.size();
@@ -1079,6 +1137,12 @@ int upload(Scene& s, int device) {
   return RTW_OK;
 }
 
+static void free_buf(DevBuf& b) {
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
 void release(Scene& s) {
   for (DeviceCopy& c : s.dev) {
     if (hipSetDevice(c.device) != hipSuccess) continue;
@@ -1086,6 +1150,10 @@ void release(Scene& s) {
     if (c.counters) hipFree(c.counters);
     if (c.sbuf) hipFree(c.sbuf);
     if (c.spill) hipFree(c.spill);
+    for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids}) free_buf(*b);
+    for (void* e : c.ev)
+      if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
+    if (c.stream) hipStreamDestroy(static_cast<hipStream_t>(c.stream));
     for (auto& e : c.kev)
       for (void* x : e)
         if (x) hipEventDestroy(static_cast<hipEvent_t>(x));
@@ -1093,10 +1161,31 @@ void release(Scene& s) {
   s.dev.clear();
 }
 
-static DeviceCopy* find_copy(Scene& s, int device) {
+DeviceCopy* find_copy(Scene& s, int device) {
   for (DeviceCopy& c : s.dev)
     if (c.device == device || device < 0) return &c;
   return nullptr;
+}
+
+int grow(DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return RTW_OK;
+  free_buf(b);
+  HIPCHK(hipMalloc(&b.p, bytes), "hipMalloc(render buffer)");
+  b.cap = bytes;
+  return RTW_OK;
+}
+
+// the scene copy's event pair (created once)
+static int copy_events(DeviceCopy& c, hipEvent_t& e0, hipEvent_t& e1) {
+  for (void*& e : c.ev)
+    if (!e) {
+      hipEvent_t x;
+      HIPCHK(hipEventCreate(&x), "hipEventCreate");
+      e = x;
+    }
+  e0 = static_cast<hipEvent_t>(c.ev[0]);
+  e1 = static_cast<hipEvent_t>(c.ev[1]);
+  return RTW_OK;
 }
 
 // Paths per pass (ordered sample buffer = 12 B per path): 2^32 = 51.5 GB of the 288 GB HBM.  A frame
@@ -1184,10 +1273,11 @@ static int resident_grid(DeviceCopy& c, path_fn fn, bool count) {
   return g;
 }
 
-static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w,
-                  uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
-                  uint32_t n_slots, float* d_out, hipStream_t stream, uint32_t flags, hipEvent_t ev0,
-                  hipEvent_t ev1) {
+int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
+                   uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles, uint32_t n_slots,
+                   float* d_out, void* stream_, uint32_t flags, void* ev0_, void* ev1_) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  hipEvent_t ev0 = static_cast<hipEvent_t>(ev0_), ev1 = static_cast<hipEvent_t>(ev1_);
   if (cam->time0 < sc.flat.time_lo || cam->time1 > sc.flat.time_hi)
     return fail(RTW_EINVAL, "camera shutter [%g, %g) outside the committed motion range [%g, %g]",
                 cam->time0, cam->time1, sc.flat.time_lo, sc.flat.time_hi);
@@ -1287,13 +1377,14 @@ static int launch(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float b
   return RTW_OK;
 }
 
-static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1, uint64_t paths,
-                      rtw_stats* st) {
-  HIPCHK(hipStreamSynchronize(stream), "render_kernel");
+int collect_stats(DeviceCopy& c, void* stream_, void* ev0_, void* ev1_, uint64_t paths, rtw_stats* st) {
+  hipEvent_t ev0 = static_cast<hipEvent_t>(ev0_), ev1 = static_cast<hipEvent_t>(ev1_);
+  HIPCHK(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "render_kernel");
   unsigned long long cnt[32];
   HIPCHK(hipMemcpy(cnt, c.counters, sizeof cnt, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
   float ms = 0.f;
   if (ev0 && ev1) HIPCHK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
+  if (cnt[30]) return fail(RTW_EINVAL, "BVH traversal guard tripped (corrupt tree?): the frame is invalid");
   st->rays = cnt[0];
   st->paths = paths;
   st->kernel_ms = ms;
@@ -1302,6 +1393,18 @@ static int fill_stats(DeviceCopy& c, hipStream_t stream, hipEvent_t ev0, hipEven
   for (int k = 0; k < 6; ++k) st->prim_tests_by_type[k] = cnt[3 + k];
   for (int k = 0; k < 6; ++k) st->simd[k] = cnt[9 + k];
   for (int k = 0; k < 4; ++k) st->phase_cycles[k] = cnt[16 + k];
+  st->boxes_tested = cnt[15];
+  st->sample_cycles = cnt[20];
+  return RTW_OK;
+}
+
+int enqueue_unpack(uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_tiles, const float* d_packed,
+                   float* d_image, void* stream) {
+  const uint32_t n = n_tiles * 64u;
+  if (!n) return RTW_OK;
+  hipLaunchKernelGGL(dev::unpack_tiles_kernel, dim3((n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     w, h, (w + 7u) / 8u, d_tiles, n_tiles, d_packed, d_image);
+  HIPCHK(hipGetLastError(), "unpack_tiles_kernel");
   return RTW_OK;
 }
 
@@ -1317,6 +1420,13 @@ int rtw_device_count(void) {
   return n;
 }
 
+// restores the caller's current device on every return path
+struct DeviceGuard {
+  int prev = 0;
+  DeviceGuard() { hipGetDevice(&prev); }
+  ~DeviceGuard() { hipSetDevice(prev); }
+};
+
 int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
                uint32_t spp, uint32_t max_depth, uint64_t seed, float* out, rtw_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
@@ -1325,27 +1435,20 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t 
   if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2 (lib.rs:84-85 divides by w-1, h-1)");
   DeviceCopy* c = find_copy(s->s, -1);
   if (!c) return fail(RTW_ENODEV, "scene has no device copy");
-  int prev = 0;
-  hipGetDevice(&prev);
+  DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-  float* d_out = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc = RTW_OK;
-  if (hipMalloc(&d_out, bytes) != hipSuccess) { hipSetDevice(prev); return fail(RTW_ENOMEM, "hipMalloc(image)"); }
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  hipEvent_t e0, e1;
+  if (int e = copy_events(*c, e0, e1)) return e;
+  if (int e = grow(c->image, bytes)) return e;  // kept for the next frame (no per-call hipMalloc)
+  float* d_out = static_cast<float*>(c->image.p);
   const uint32_t n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
   rtw_stats st;
   memset(&st, 0, sizeof st);
-  rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, nullptr, n_tiles, d_out, nullptr, 0, e0, e1);
-  if (rc == RTW_OK) rc = fill_stats(*c, nullptr, e0, e1, (uint64_t)w * h * spp, &st);
+  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, nullptr, n_tiles, d_out, nullptr, 0, e0, e1);
+  if (rc == RTW_OK) rc = collect_stats(*c, nullptr, e0, e1, (uint64_t)w * h * spp, &st);
   if (rc == RTW_OK && hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(RTW_ENODEV, "hipMemcpy(image)");
-  hipFree(d_out);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipSetDevice(prev);
   st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = st;
   return rc;
@@ -1353,7 +1456,7 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t 
 
 int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w,
                       uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
-                      uint32_t n_tiles, float* d_out, void* stream_, uint32_t flags, rtw_stats* stats) {
+                      uint32_t n_tiles, float* d_out, void* stream, uint32_t flags, rtw_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!s || !cam || !bg || !d_out) return fail(RTW_EINVAL, "NULL argument");
   if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
@@ -1361,23 +1464,19 @@ int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const flo
   DeviceCopy* c = find_copy(s->s, device);
   if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
   if (!d_tiles) n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
-  int prev = 0;
-  hipGetDevice(&prev);
+  DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  hipStream_t stream = (hipStream_t)stream_;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (stats) { hipEventCreate(&e0); hipEventCreate(&e1); }
-  int rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_tiles, n_tiles, d_out, stream, flags, e0, e1);
+  if (stats)
+    if (int e = copy_events(*c, e0, e1)) return e;
+  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_tiles, n_tiles, d_out, stream, flags, e0, e1);
   if (rc == RTW_OK && stats) {
     rtw_stats st;
     memset(&st, 0, sizeof st);
-    rc = fill_stats(*c, stream, e0, e1, (uint64_t)n_tiles * 64u * spp, &st);
+    rc = collect_stats(*c, stream, e0, e1, (uint64_t)n_tiles * 64u * spp, &st);
     st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *stats = st;
   }
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  hipSetDevice(prev);
   return rc;
 }
 
@@ -1392,35 +1491,31 @@ int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], ui
   if (!c) return fail(RTW_ENODEV, "scene has no device copy");
   const uint32_t tiles_x = (w + 7u) / 8u, tiles_y = (h + 7u) / 8u;
   const uint32_t band_ty = std::max(1u, ((band_rows ? band_rows : 64u) + 7u) / 8u);  // tile rows per band
-  int prev = 0;
-  hipGetDevice(&prev);
+  DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   std::vector<uint32_t> ids((size_t)tiles_x * tiles_y);
   for (uint32_t k = 0; k < ids.size(); ++k) ids[k] = k;  // tile row ty = output rows [8 ty, 8 ty + 8)
-  uint32_t* d_ids = nullptr;
-  float* d_packed = nullptr;
   const size_t band_tiles = (size_t)band_ty * tiles_x;
+  if (int e = grow(c->tiles, ids.size() * sizeof(uint32_t))) return e;
+  if (int e = grow(c->packed, band_tiles * 64 * 3 * sizeof(float))) return e;
+  uint32_t* d_ids = static_cast<uint32_t*>(c->tiles.p);
+  float* d_packed = static_cast<float*>(c->packed.p);
+  hipEvent_t e0, e1;
+  if (int e = copy_events(*c, e0, e1)) return e;
   int rc = RTW_OK;
-  if (hipMalloc((void**)&d_ids, ids.size() * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&d_packed, band_tiles * 64 * 3 * sizeof(float)) != hipSuccess) {
-    rc = fail(RTW_ENOMEM, "hipMalloc(stream buffers)");
-  } else if (hipMemcpy(d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMemcpy(d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(RTW_ENODEV, "hipMemcpy(tile ids)");
-  }
   std::vector<float> packed(band_tiles * 64 * 3);
   std::vector<rtw_pixel> px;
   rtw_stats tot;
   memset(&tot, 0, sizeof tot);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
   for (uint32_t ty0 = 0; rc == RTW_OK && ty0 < tiles_y; ty0 += band_ty) {
     const uint32_t nty = std::min(band_ty, tiles_y - ty0), nt = nty * tiles_x;
-    rc = launch(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_ids + (size_t)ty0 * tiles_x, nt, d_packed, nullptr,
-                0, e0, e1);
+    rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_ids + (size_t)ty0 * tiles_x, nt, d_packed,
+                        nullptr, 0, e0, e1);
     rtw_stats st;
     memset(&st, 0, sizeof st);
-    if (rc == RTW_OK) rc = fill_stats(*c, nullptr, e0, e1, 0, &st);
+    if (rc == RTW_OK) rc = collect_stats(*c, nullptr, e0, e1, 0, &st);
     if (rc == RTW_OK && hipMemcpy(packed.data(), d_packed, (size_t)nt * 64 * 3 * sizeof(float),
                                   hipMemcpyDeviceToHost) != hipSuccess)
       rc = fail(RTW_ENODEV, "hipMemcpy(band)");
@@ -1438,11 +1533,6 @@ int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], ui
       }
     if (int e = sink(px.data(), (uint32_t)px.size(), user)) rc = e;
   }
-  if (d_ids) hipFree(d_ids);
-  if (d_packed) hipFree(d_packed);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipSetDevice(prev);
   tot.paths = (uint64_t)w * h * spp;
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = tot;
@@ -1500,19 +1590,9 @@ int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out
 int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_tiles,
                             const float* d_packed, float* d_image, void* stream) {
   if (!d_tiles || !d_packed || !d_image) return fail(RTW_EINVAL, "NULL argument");
-  int prev = 0;
-  hipGetDevice(&prev);
+  DeviceGuard g;
   if (device >= 0) HIPCHK(hipSetDevice(device), "hipSetDevice");
-  const uint32_t n = n_tiles * 64u;
-  if (n) {
-    hipLaunchKernelGGL(dev::unpack_tiles_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, h,
-                       (w + 7u) / 8u, d_tiles, n_tiles, d_packed, d_image);
-    hipError_t e = hipGetLastError();
-    hipSetDevice(prev);
-    if (e != hipSuccess) return hip_fail(e, "unpack_tiles_kernel");
-  }
-  hipSetDevice(prev);
-  return RTW_OK;
+  return enqueue_unpack(w, h, d_tiles, n_tiles, d_packed, d_image, stream);
 }
 
 }  // extern "C"

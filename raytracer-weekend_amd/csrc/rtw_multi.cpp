@@ -1,0 +1,236 @@
+// rtw_multi.cpp — Raytracer::render() over the GPUs of one node from ONE host thread.
+//
+// The reference's only parallelism is Rayon over the pixels of a frame (raytracer_weekend_lib/src/
+// lib.rs:57-76).  Here the frame's 8x8 pixel tiles are dealt round-robin to n_gpus devices (tile k ->
+// device k mod n; rtw_tile_partition), every device renders its tiles into a packed buffer on its
+// own stream with its own copy of the scene (rtw_scene_commit uploads one per device), and one RCCL
+// gather over xGMI — a grouped ncclSend from every device to device 0 / ncclRecv on device 0 (RCCL
+// has no Gather collective) — brings the packed tiles to device 0, which scatters them into the
+// frame and copies it to the host.  Pixels depend only on (seed, j, i, sample), so the frame is
+// bit-identical to rtw_render's for every n_gpus.
+//
+// RCCL is opened at the first multi-device render (dlopen of librccl.so.1), so the rest of the
+// library does not depend on it.
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <chrono>
+#include <vector>
+
+#include "../../include/rtw.h"
+#include "rtw_scene.hpp"
+
+namespace rtw {
+namespace {
+
+struct Rccl {
+  bool tried = false;
+  void* h = nullptr;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+  static Rccl r;
+  if (r.tried) return r;
+  r.tried = true;
+  for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+    r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+    if (r.h) break;
+  }
+  if (!r.h) return r;
+  auto sym = [&](auto& fn, const char* n) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r.h, n)); };
+  sym(r.comm_init_all, "ncclCommInitAll");
+  sym(r.comm_destroy, "ncclCommDestroy");
+  sym(r.send, "ncclSend");
+  sym(r.recv, "ncclRecv");
+  sym(r.group_start, "ncclGroupStart");
+  sym(r.group_end, "ncclGroupEnd");
+  sym(r.error_string, "ncclGetErrorString");
+  if (!r.comm_init_all || !r.comm_destroy || !r.send || !r.recv || !r.group_start || !r.group_end || !r.error_string) {
+    dlclose(r.h);
+    r.h = nullptr;
+  }
+  return r;
+}
+
+// one communicator clique per device count, kept for the process (ncclCommInitAll is slow)
+struct Clique {
+  int n = 0;
+  std::vector<ncclComm_t> comms;
+};
+std::vector<Clique>& cliques() {
+  static std::vector<Clique> c;
+  return c;
+}
+
+#define HIPOK(x, what)                                                              \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) return fail(RTW_ENODEV, "%s: %s", what, hipGetErrorString(e_)); \
+  } while (0)
+#define NCCLOK(x, what)                                                                       \
+  do {                                                                                        \
+    ncclResult_t r_ = (x);                                                                    \
+    if (r_ != ncclSuccess) return fail(RTW_ENODEV, "%s: %s", what, rccl().error_string(r_)); \
+  } while (0)
+
+int get_clique(int n, std::vector<ncclComm_t>** out) {
+  for (Clique& c : cliques())
+    if (c.n == n) {
+      *out = &c.comms;
+      return RTW_OK;
+    }
+  Rccl& r = rccl();
+  if (!r.h) return fail(RTW_ENODEV, "librccl.so.1 not loadable (multi-device gather needs RCCL)");
+  Clique c;
+  c.n = n;
+  c.comms.resize(n);
+  std::vector<int> devs(n);
+  for (int d = 0; d < n; ++d) devs[d] = d;
+  NCCLOK(r.comm_init_all(c.comms.data(), n, devs.data()), "ncclCommInitAll");
+  cliques().push_back(c);
+  *out = &cliques().back().comms;
+  return RTW_OK;
+}
+
+}  // namespace
+}  // namespace rtw
+
+using namespace rtw;
+
+extern "C" {
+
+int rtw_tile_partition(uint32_t w, uint32_t h, uint32_t n_parts, uint32_t part, uint32_t* ids, uint32_t cap,
+                       uint32_t* n_ids) {
+  if (!n_ids || n_parts == 0 || part >= n_parts || (cap && !ids)) return fail(RTW_EINVAL, "bad arguments");
+  const uint32_t nt = ((w + 7u) / 8u) * ((h + 7u) / 8u), per = (nt + n_parts - 1) / n_parts;
+  uint32_t k = 0;
+  for (uint32_t t = part; t < nt; t += n_parts, ++k)
+    if (k < cap) ids[k] = t;
+  for (uint32_t q = k; q < per && q < cap; ++q) ids[q] = nt;  // padding up to the common size
+  *n_ids = k;
+  return RTW_OK;
+}
+
+int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
+                     uint32_t spp, uint32_t max_depth, uint64_t seed, float* out, rtw_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!s || !cam || !bg || !out) return fail(RTW_EINVAL, "NULL argument");
+  if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
+  if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2 (lib.rs:84-85 divides by w-1, h-1)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
+  const int n = n_gpus <= 0 ? ndev : n_gpus;
+  if (n > ndev) return fail(RTW_EINVAL, "n_gpus %d > visible devices %d", n_gpus, ndev);
+  std::vector<DeviceCopy*> cp(n);
+  for (int d = 0; d < n; ++d) {
+    cp[d] = nullptr;
+    for (DeviceCopy& c : s->s.dev)
+      if (c.device == d) cp[d] = &c;
+    if (!cp[d]) return fail(RTW_ENODEV, "scene was not committed to device %d (commit with device = -1)", d);
+  }
+  std::vector<ncclComm_t>* comms = nullptr;
+  if (int e = get_clique(n, &comms)) return e;
+  Rccl& r = rccl();
+  int prev = 0;
+  hipGetDevice(&prev);
+  struct Restore {
+    int d;
+    ~Restore() { hipSetDevice(d); }
+  } restore{prev};
+
+  const uint32_t tiles_x = (w + 7u) / 8u, nt = tiles_x * ((h + 7u) / 8u);
+  const uint32_t per = (nt + (uint32_t)n - 1) / (uint32_t)n;  // padded tiles per device
+  const size_t slot_floats = (size_t)per * 64 * 3;
+  std::vector<uint32_t> ids(per), all((size_t)n * per);
+  std::vector<uint32_t> mine(n);
+  for (int d = 0; d < n; ++d) rtw_tile_partition(w, h, (uint32_t)n, (uint32_t)d, all.data() + (size_t)d * per, per, &mine[d]);
+
+  // 1. every device renders its tiles on its own stream (all enqueued before any wait)
+  std::vector<hipEvent_t> e0(n), e1(n);
+  for (int d = 0; d < n; ++d) {
+    DeviceCopy& c = *cp[d];
+    HIPOK(hipSetDevice(d), "hipSetDevice");
+    if (!c.stream) {
+      hipStream_t st;
+      HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+      c.stream = st;
+    }
+    for (void*& e : c.ev)
+      if (!e) {
+        hipEvent_t x;
+        HIPOK(hipEventCreate(&x), "hipEventCreate");
+        e = x;
+      }
+    e0[d] = static_cast<hipEvent_t>(c.ev[0]);
+    e1[d] = static_cast<hipEvent_t>(c.ev[1]);
+    hipStream_t st = static_cast<hipStream_t>(c.stream);
+    if (int e = grow(c.tiles, per * sizeof(uint32_t))) return e;
+    if (int e = grow(c.packed, slot_floats * sizeof(float))) return e;
+    HIPOK(hipMemcpyAsync(c.tiles.p, all.data() + (size_t)d * per, per * sizeof(uint32_t), hipMemcpyHostToDevice, st),
+          "hipMemcpyAsync(tile ids)");
+    if (int e = enqueue_render(s->s, c, cam, bg, w, h, spp, max_depth, seed, static_cast<uint32_t*>(c.tiles.p), mine[d],
+                               static_cast<float*>(c.packed.p), st, 0, e0[d], e1[d]))
+      return e;
+  }
+  // 2. one RCCL gather to device 0 (each device's send waits for its render on the same stream)
+  DeviceCopy& c0 = *cp[0];
+  HIPOK(hipSetDevice(0), "hipSetDevice");
+  hipStream_t st0 = static_cast<hipStream_t>(c0.stream);
+  if (int e = grow(c0.gathered, (size_t)n * slot_floats * sizeof(float))) return e;
+  if (int e = grow(c0.gather_ids, all.size() * sizeof(uint32_t))) return e;
+  if (int e = grow(c0.image, (size_t)w * h * 3 * sizeof(float))) return e;
+  HIPOK(hipMemcpyAsync(c0.gather_ids.p, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st0),
+        "hipMemcpyAsync(gather ids)");
+  float* gathered = static_cast<float*>(c0.gathered.p);
+  NCCLOK(r.group_start(), "ncclGroupStart");
+  for (int d = 0; d < n; ++d) {
+    hipStream_t st = static_cast<hipStream_t>(cp[d]->stream);
+    const ncclResult_t a = r.send(cp[d]->packed.p, slot_floats, ncclFloat32, 0, (*comms)[d], st);
+    if (a != ncclSuccess) {
+      r.group_end();
+      return fail(RTW_ENODEV, "ncclSend: %s", r.error_string(a));
+    }
+  }
+  for (int d = 0; d < n; ++d) {
+    const ncclResult_t a = r.recv(gathered + (size_t)d * slot_floats, slot_floats, ncclFloat32, d, (*comms)[0], st0);
+    if (a != ncclSuccess) {
+      r.group_end();
+      return fail(RTW_ENODEV, "ncclRecv: %s", r.error_string(a));
+    }
+  }
+  NCCLOK(r.group_end(), "ncclGroupEnd");
+  // 3. device 0 scatters the gathered tiles into the frame and copies it out
+  HIPOK(hipSetDevice(0), "hipSetDevice");
+  if (int e = enqueue_unpack(w, h, static_cast<uint32_t*>(c0.gather_ids.p), (uint32_t)all.size(), gathered,
+                             static_cast<float*>(c0.image.p), st0))
+    return e;
+  HIPOK(hipMemcpyAsync(out, c0.image.p, (size_t)w * h * 3 * sizeof(float), hipMemcpyDeviceToHost, st0),
+        "hipMemcpyAsync(image)");
+  rtw_stats tot;
+  memset(&tot, 0, sizeof tot);
+  for (int d = 0; d < n; ++d) {
+    HIPOK(hipSetDevice(d), "hipSetDevice");
+    rtw_stats st;
+    memset(&st, 0, sizeof st);
+    if (int e = collect_stats(*cp[d], cp[d]->stream, e0[d], e1[d], 0, &st)) return e;
+    tot.rays += st.rays;
+    tot.kernel_ms = std::max(tot.kernel_ms, st.kernel_ms);  // the devices run concurrently
+  }
+  tot.paths = (uint64_t)w * h * spp;
+  tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) *stats = tot;
+  return RTW_OK;
+}
+
+}  // extern "C"

@@ -191,13 +191,14 @@ extern "C" int rtw_load_wavefront_obj(rtw_scene* s, const char* path, rtw_image_
     if (mtllib.empty()) return fail(RTW_EIO, "%s: usemtl without mtllib (triangular.rs:176 unwrap)", path);
     if (int e = parse_mtl(dir_of(path) + "/" + mtllib, mtl)) return e;
   }
+  // every material is resolved before the BvhNode group opens, so a parse / texture error leaves
+  // the caller's scene without a dangling open group
   std::map<std::string, uint32_t> mat_ids;
   uint32_t magenta = UINT32_MAX;
-  uint32_t total = 0;
-  if (int e = rtw_begin_bvh(s, 0.0f, 1.0f)) return e;
-  for (const FaceSet& fs : sets) {
-    uint32_t n = (uint32_t)fs.nm.size();
-    if (!n) continue;
+  std::vector<uint32_t> set_mat(sets.size(), UINT32_MAX);
+  for (size_t q = 0; q < sets.size(); ++q) {
+    const FaceSet& fs = sets[q];
+    if (fs.nm.empty()) continue;
     uint32_t mat;
     if (fallback_material != UINT32_MAX) {
       mat = fallback_material;
@@ -231,8 +232,18 @@ extern "C" int rtw_load_wavefront_obj(rtw_scene* s, const char* path, rtw_image_
         mat_ids[fs.material] = mat;
       }
     }
-    if (int e = rtw_add_triangles(s, n, fs.v.data(), fs.n.data(), fs.nm.data(), fs.uv.data(), fs.um.data(), mat))
+    set_mat[q] = mat;
+  }
+  uint32_t total = 0;
+  if (int e = rtw_begin_bvh(s, 0.0f, 1.0f)) return e;
+  for (size_t q = 0; q < sets.size(); ++q) {
+    const FaceSet& fs = sets[q];
+    const uint32_t n = (uint32_t)fs.nm.size();
+    if (!n) continue;
+    if (int e = rtw_add_triangles(s, n, fs.v.data(), fs.n.data(), fs.nm.data(), fs.uv.data(), fs.um.data(), set_mat[q])) {
+      rtw_end(s);  // close the group: the caller sees this error, not "group(s) still open" at commit
       return e;
+    }
     total += n;
   }
   if (int e = rtw_end(s)) return e;
@@ -274,8 +285,10 @@ int load_rtwm(rtw_scene* hs, const char* path, uint32_t mat, uint32_t* ntri_out)
   }
   if (int e = rtw_begin_bvh(hs, 0.0f, 1.0f)) return e;
   if (int e = rtw_add_triangles(hs, n, v.data(), (flags & 1) ? nn.data() : nullptr, (flags & 1) ? nm.data() : nullptr,
-                                (flags & 2) ? uv.data() : nullptr, (flags & 2) ? um.data() : nullptr, mat))
+                                (flags & 2) ? uv.data() : nullptr, (flags & 2) ? um.data() : nullptr, mat)) {
+    rtw_end(hs);  // close the group (see rtw_load_wavefront_obj)
     return e;
+  }
   if (int e = rtw_end(hs)) return e;
   if (ntri_out) *ntri_out = n;
   return RTW_OK;

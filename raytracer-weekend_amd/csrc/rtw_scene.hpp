@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/rtw.h"
 #include "rtw_device.hpp"
 
 struct rtw_scene;  // opaque in the C-ABI; defined below as rtw::Scene's holder
@@ -58,6 +59,7 @@ struct Flat {
   std::vector<DevNode4> nodes4;  // what the kernel walks
   uint32_t stack_need = 0;       // worst-case traversal stack entries of nodes4
   std::vector<DevPrim> prims;
+  std::vector<DevShade> shade;  // per prim: material + common texture values (rtw_device.hpp)
   std::vector<uint32_t> always;
   std::vector<DevTriShade> tshade;
   std::vector<DevInst> insts;
@@ -70,12 +72,17 @@ struct Flat {
   float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover
 };
 
+struct DevBuf {  // a grow-only device allocation
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
 struct DeviceCopy {
   int device = -1;
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
-  unsigned long long* counters = nullptr;  // 32 x u64: [0..19] stats, [31] path queue
+  unsigned long long* counters = nullptr;  // 32 x u64: [0..19] stats, [30] traversal error flag, [31] path queue
   float* sbuf = nullptr;                   // ordered per-sample radiance (rgb per path)
   uint64_t sbuf_paths = 0;
   int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)
@@ -85,6 +92,11 @@ struct DeviceCopy {
   uint32_t kev_head = 0, kev_count = 0;
   int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting); the
                                            // variant is fixed per scene (features)
+  // device buffers kept across render calls (grown, never shrunk; freed by release()): a
+  // 30-camera animation through rtw_render does no hipMalloc after the first frame
+  DevBuf image, tiles, packed, gathered, gather_ids;
+  void* ev[2] = {nullptr, nullptr};        // hipEvent_t pair timing rtw_render / multi calls
+  void* stream = nullptr;                  // hipStream_t of rtw_render_multi on this device
 };
 
 struct Scene {
@@ -107,6 +119,17 @@ std::string dump_scene(const Scene& s);
 // rtw_kernel.hip
 int upload(Scene& s, int device);
 void release(Scene& s);
+DeviceCopy* find_copy(Scene& s, int device);  // device < 0: the first copy
+int grow(DevBuf& b, size_t bytes);            // current device; contents not kept
+// enqueue one render (path kernel passes + in-order reductions) on `stream` (hipStream_t) of
+// c.device, which must be current; d_tiles == nullptr renders every tile into a full image
+int enqueue_render(Scene& s, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
+                   uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles, uint32_t n_tiles,
+                   float* d_out, void* stream, uint32_t flags, void* ev0, void* ev1);
+// wait for `stream`, read the launch counters and the ev0 -> ev1 time into st
+int collect_stats(DeviceCopy& c, void* stream, void* ev0, void* ev1, uint64_t paths, rtw_stats* st);
+int enqueue_unpack(uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_tiles, const float* d_packed,
+                   float* d_image, void* stream);
 
 // thread-local error reporting (rtw_capi.cpp)
 int fail(int code, const char* fmt, ...);

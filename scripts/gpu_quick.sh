@@ -5,7 +5,7 @@ TAG=${TAG:-q_}
 cd $R
 mkdir -p gpurun_out
 if [ -z "$NOTEST" ]; then
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > gpurun_out/${TAG}pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}pytest.log; exit 1; }
 tail -1 gpurun_out/${TAG}pytest.log
 fi
 for c in ${CONFIGS:-jumpy-1080p cornell-800 cow-1080p monument-4k}; do

@@ -42,3 +42,23 @@ def test_obj_reference_material_rules(rtw, tmp_path):
     assert s.load_wavefront_obj(tmp_path / "d.obj") == 1  # negative (relative) indices
     tri = [l for l in s.dump().splitlines() if l.startswith("tri")][0].split()
     assert tri[10] == "7"  # all three vertex normals present
+
+
+def test_obj_error_leaves_no_open_group(rtw, tmp_path):
+    """A material error (missing map_Kd loader, material not in the MTL) is reported by the loader
+    and leaves the caller's scene with no open BvhNode group: a later commit fails for its own
+    reason (no device here / succeeds on the GPU box), never with "group(s) still open"."""
+    (tmp_path / "c.mtl").write_text("newmtl x\nillum 1\nmap_Kd missing.png\n")
+    (tmp_path / "c.obj").write_text("mtllib c.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvt 0 0\nvt 1 0\nvt 0 1\n"
+                                    "usemtl x\nf 1/1 2/2 3/3\nusemtl y\nf 1/1 2/2 3/3\n")
+    s = rtw.Scene()
+    m = s.lambertian_solid((0.5, 0.5, 0.5))
+    s.sphere((0, 0, 0), 1, m)
+    with pytest.raises(rtw.RtwError) as e:
+        s.load_wavefront_obj(tmp_path / "c.obj")
+    assert e.value.code == rtw.RTW_EIO
+    assert "begin bvh" not in s.dump()
+    try:
+        s.commit()
+    except rtw.RtwError as err:
+        assert err.code == rtw.RTW_ENODEV, err

@@ -220,17 +220,34 @@ def test_render_stream_pixels(gpu):
 
 
 def test_console_app_frames(gpu, tmp_path):
-    """console_app/src/main.rs:28-94: one PNG per camera (30 for animated-book2-final-scene),
-    each the tonemapped render of that camera over the one committed world."""
+    """console_app/src/main.rs:28-94: one PNG per camera (30 for animated-book2-final-scene), named
+    render/image_{:04}.png (:92-94), each the tonemap (:68-90) of that camera's render over the one
+    committed world, rows top-down = the emission order row j = h-1 .. 0 (:66-71).  The PNG pixels
+    are decoded and compared byte for byte with rtw_tonemap(rtw_render(...)) for three cameras."""
     import subprocess
     from pathlib import Path
+    from PIL import Image
+    rtw = gpu
     exe = Path(__file__).resolve().parents[1] / "raytracer-weekend_amd" / "bin" / "rtw_console"
     assert exe.exists(), "rtw_console not built"
-    r = subprocess.run([str(exe), "animated-book2-final-scene", "-w", "32", "-a", "1.7777778", "-s", "2",
+    name, width, aspect, spp, seed = "animated-book2-final-scene", 32, 1.7777778, 2, 0
+    r = subprocess.run([str(exe), name, "-w", str(width), "-a", str(aspect), "-s", str(spp),
                         "--models", str(gpu.MODELS_DIR), "--out", str(tmp_path)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     pngs = sorted(tmp_path.glob("image_*.png"))
     assert [p.name for p in pngs] == [f"image_{k:04d}.png" for k in range(30)]
-    assert all(p.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n" for p in pngs)
     assert len(set(p.read_bytes() for p in pngs)) > 20  # the camera sweeps across the scene
+    height = rtw.image_height(width, aspect)            # main.rs:33
+    cam_aspect = rtw.camera_aspect(width, height)       # main.rs:38-41
+    s = rtw.Scene()
+    _, bg = s.preset(name, cam_aspect, seed=seed)
+    s.commit()
+    cams = rtw.preset_cameras(name, cam_aspect)
+    assert len(cams) == 30
+    for k in (0, 13, 29):
+        sums, _ = rtw.Raytracer(s, cams[k], bg, width, height, spp, seed=seed).render()
+        want = rtw.tonemap(sums, spp)
+        got = np.asarray(Image.open(pngs[k]).convert("RGB"))
+        assert got.shape == (height, width, 3)
+        assert np.array_equal(got, want), f"camera {k}: {int((got != want).sum())} bytes differ"

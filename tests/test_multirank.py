@@ -93,3 +93,39 @@ def test_partition_covers_every_tile_once():
             assert np.array_equal(real, np.arange(nt))
             sizes = [len(tiles.rank_tiles(nt, world, r)) for r in range(world)]
             assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 800), (17, 9)])
+def test_c_abi_tile_partition_and_gather_layout(rtw, n, w, h):
+    """rtw_tile_partition (what rtw_render_multi deals to each device) is the round-robin
+    partition of tiles.py; the rank-major padded gather buffer that device 0 receives from the
+    RCCL send/recv group, unpacked with unpack_tiles_kernel's index math, rebuilds the frame."""
+    import importlib
+    tiles = importlib.import_module("rtw_amd.tiles")
+    nt = rtw.n_tiles(w, h)
+    per = (nt + n - 1) // n
+    parts = [rtw.tile_partition(w, h, n, p) for p in range(n)]
+    assert all(len(ids) == per for ids, _ in parts)
+    layout = np.concatenate([ids for ids, _ in parts]).astype(np.int64)
+    assert np.array_equal(layout, tiles.gather_layout(nt, n))
+    assert sum(k for _, k in parts) == nt and max(k for _, k in parts) - min(k for _, k in parts) <= 1
+    real = layout[layout < nt]
+    assert np.array_equal(np.sort(real), np.arange(nt))
+    if w * h > 1_000_000:
+        return  # layout checked; the pixel scatter below is exercised on the small frames
+    gathered = np.zeros((n * per, 64, 3), np.float32)
+    for slot, t in enumerate(layout):
+        if t < nt:
+            r, c = tiles.tile_pixels(int(t), w, h)
+            gathered[slot] = fake_pixel(r, c)
+    img = unpack(w, h, layout, gathered)
+    rows, cols = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    assert np.array_equal(img, fake_pixel(rows, cols))
+
+
+def test_c_abi_tile_partition_errors(rtw):
+    with pytest.raises(rtw.RtwError):
+        rtw.tile_partition(64, 64, 0, 0)
+    with pytest.raises(rtw.RtwError):
+        rtw.tile_partition(64, 64, 2, 2)
