@@ -19,21 +19,9 @@
 namespace rtw {
 
 // T[0] holds the weights 2^31 .. 2^0 of 1/pi (zero); T[k] (k >= 1) the weights 2^(31-32k) .. 2^(-32k).
-RTW_HD uint32_t inv_pi_word(int k) {
-  switch (k) {
-    case 1: return 0x517CC1B7u;
-    case 2: return 0x27220A94u;
-    case 3: return 0xFE13ABE8u;
-    case 4: return 0xFA9A6EE0u;
-    case 5: return 0x6DB14ACCu;
-    case 6: return 0x9E21C820u;
-    case 7: return 0xFF28B1D5u;
-    case 8: return 0xEF5DE2B0u;
-    case 9: return 0xDB92371Du;
-    case 10: return 0x2126E970u;
-    default: return 0u;
-  }
-}
+constexpr uint32_t INV_PI_T[12] = {0u,          0x517CC1B7u, 0x27220A94u, 0xFE13ABE8u, 0xFA9A6EE0u, 0x6DB14ACCu,
+                                   0x9E21C820u, 0xFF28B1D5u, 0xEF5DE2B0u, 0xDB92371Du, 0x2126E970u, 0u};
+RTW_HD uint32_t inv_pi_word(int k) { return (k >= 0 && k < 12) ? INV_PI_T[k] : 0u; }
 // 32 bits of T starting at bit index b (index 0 = weight 2^31)
 RTW_HD uint32_t inv_pi_bits32(int b) {
   const int q = b >> 5, s = b & 31;

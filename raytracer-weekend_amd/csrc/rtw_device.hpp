@@ -131,7 +131,11 @@ enum Feature : uint32_t {
   F_NOISE = 1u << 14,   // Perlin noise textures
   F_ISO = 1u << 15,     // Isotropic materials
 };
-constexpr uint32_t F_ALL = (1u << 16) - 1;
+// Not a primitive / material kind: some material's texture needs the generic texture walk
+// (image, noise, uv-debug, nested checkers; DevShade SM_GENERIC).  Scenes with only solid and
+// checker(solid, solid) textures get kernels without it.
+constexpr uint32_t F_TEXGEN = 1u << 17;
+constexpr uint32_t F_ALL = ((1u << 16) - 1) | F_TEXGEN;
 // Kernel-only flag (not a scene feature): the world has no BVH (list mode, rtw_flatten.cpp), so
 // the variant compiles without the BVH walk and its registers (higher occupancy).
 constexpr uint32_t F_LIST = 1u << 16;
@@ -141,7 +145,7 @@ constexpr uint32_t F_LIST = 1u << 16;
 constexpr uint32_t F_SPHERES = F_SPHERE | F_MSPHERE | F_CHECKER | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
 constexpr uint32_t F_BOXES = F_RECT | F_INST | F_LAMBERT | F_METAL | F_DIEL | F_LIGHT;
 constexpr uint32_t F_SMOKE = F_BOXES | F_MEDIUM | F_ISO;  // smokey-cornell-box
-constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F_IMAGE | F_LAMBERT | F_LIGHT;
+constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F_IMAGE | F_LAMBERT | F_LIGHT | F_TEXGEN;
 
 struct DevScene {
   const DevNode4* nodes;

@@ -607,6 +607,7 @@ int flatten(Scene& s) {
     }
     d.kind = m.type | (mode << 8) | (m.needs_uv ? 1u << 12 : 0u);
     f.shade.push_back(d);
+    if (mode == SM_GENERIC) f.features |= F_TEXGEN;
   }
   // 4-wide tree for the kernel
   if (!f.nodes.empty()) {
@@ -655,7 +656,7 @@ int flatten(Scene& s) {
   for (const DevTex& t : f.texs)
     F |= t.type == TT_CHECKER ? F_CHECKER : t.type == TT_IMAGE ? F_IMAGE : t.type == TT_UVDEBUG ? F_UVDEBUG :
          t.type == TT_NOISE ? F_NOISE : 0u;
-  f.features = F;
+  f.features |= F;
   // structural self-check: every internal node reached exactly once from the root, every
   // leaf range inside the BVH part of prims[], every BVH prim covered exactly once
   if (!f.nodes.empty()) {

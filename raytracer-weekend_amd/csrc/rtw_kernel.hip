@@ -669,35 +669,22 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
 // sign(sinf x) = parity of floor(x / pi), by the double-precision product for 2^-12 <= |x| < 65536
 // and by the exact integer reduction rtw::pi_parity for |x| >= 65536; sinf x == x for |x| < 2^-12;
 // |sinf x| >= 3.2e-9 for |x| >= 2^-12 (no product of three such factors underflows).  So the
-// decision is the XOR of the factors' signs, except that NaN / inf / 0 factors give "even", and a
-// product with tiny factors below 2^-120 (some |f x| < ~1e-20) is evaluated literally with the
-// correctly rounded dev_sinf (glibc's sinf is <= 1 ulp off: that corner alone is not pinned).
+// decision is the XOR of the factors' signs, except that NaN / inf / 0 factors give "even" and a
+// product that underflows to zero is "even".  Underflow needs a tiny factor: it is decided from the
+// product of the tiny factors alone (|sin| of the others taken as 1), exact unless that product is
+// below 2^-120 / 3.2e-9^k (some |f x| < ~1e-20): that corner alone is not pinned.
 __device__ __forceinline__ bool checker_odd_slow(float fx, float fy, float fz) {
   const float f[3] = {fx, fy, fz};
   uint32_t neg = 0;
-  double lower = 1.0;  // lower bound of |product|
-  bool tiny = false;
-  for (int k = 0; k < 3; ++k) {
-    const float x = f[k];
-    if (x != x || isinf(x) || x == 0.0f) return false;  // NaN or +-0 product: `< 0` is false
-    const float ax = fabsf(x);
-    if (ax < 0x1p-12f) {
-      neg ^= x < 0.0f ? 1u : 0u;
-      lower *= (double)ax;
-      tiny = true;
-    } else {
-      neg ^= pi_parity(ax) ^ (x < 0.0f ? 1u : 0u);
-      lower *= 3.2e-9;
-    }
-  }
-  if (!tiny || lower >= 0x1p-120) return neg != 0;
-  float p = 1.0f;  // the literal left-to-right product (underflow corner)
+  float tiny = 1.0f;  // left-to-right product of the tiny factors (sinf x == x there)
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float x = f[k], ax = fabsf(x);
-    const float s = ax < 0x1p-12f ? x : (ax < 1048576.0f ? dev_sinf(x) : (((pi_parity(ax) ^ (x < 0.0f)) & 1u) ? -1.0f : 1.0f));
-    p = p * s;
+    if (x != x || isinf(x) || x == 0.0f) return false;  // NaN or +-0 product: `< 0` is false
+    if (ax < 0x1p-12f) tiny = tiny * ax;
+    neg ^= (ax < 0x1p-12f ? 0u : pi_parity(ax)) ^ (x < 0.0f ? 1u : 0u);
   }
-  return p < 0.0f;
+  return neg != 0 && tiny != 0.0f;
 }
 __device__ __forceinline__ bool checker_odd(float fx, float fy, float fz) {
   const float ax = fabsf(fx), ay = fabsf(fy), az = fabsf(fz);
@@ -983,7 +970,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
         if (mode == SM_SOLID) att = ld3(sh.a);  // SolidColor::value
         else if ((FEAT & F_CHECKER) && mode == SM_CHECKER)
           att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a) : ld3(sh.b);
-        else att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
+        else if (FEAT & F_TEXGEN) att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
       }
       if (light) {  // emit, no scatter
         L = mul(st.T, att);
