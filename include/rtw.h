@@ -66,10 +66,11 @@ typedef struct {
    * traversal and shading, and in the whole path kernel, summed over waves */
   uint64_t phase_cycles[4];
   /* RTW_FLAG_COUNT_TRAVERSAL: child boxes slab-tested (the non-empty slots of the visited 4-wide
-   * nodes), and the wave-cycles of shading spent in random_in_unit_sphere (part of phase_cycles[2]'s
-   * shading time, counted apart from it) */
+   * nodes), and sub-phase wave-cycles: [0] shading's random_in_unit_sphere (counted apart from
+   * phase_cycles[2]), [1] traversal's node loop and [2] leaf tests (parts of phase_cycles[1]),
+   * [3] regeneration's per-lane path start (part of phase_cycles[0]) */
   uint64_t boxes_tested;
-  uint64_t sample_cycles;
+  uint64_t sub_cycles[4];
 } rtw_stats;
 
 enum { RTW_FLAG_COUNT_TRAVERSAL = 1 };

@@ -52,7 +52,7 @@ class rtw_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("kernel_ms", C.c_double),
                 ("total_ms", C.c_double), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("prim_tests_by_type", C.c_uint64 * 6), ("simd", C.c_uint64 * 6),
-                ("phase_cycles", C.c_uint64 * 4), ("boxes_tested", C.c_uint64), ("sample_cycles", C.c_uint64)]
+                ("phase_cycles", C.c_uint64 * 4), ("boxes_tested", C.c_uint64), ("sub_cycles", C.c_uint64 * 4)]
 
     def as_dict(self) -> dict:
         return {"rays": int(self.rays), "paths": int(self.paths), "kernel_ms": float(self.kernel_ms),
@@ -64,7 +64,8 @@ class rtw_stats(C.Structure):
                 "boxes_tested": int(self.boxes_tested),
                 "phase_share": dict({k: (self.phase_cycles[q] / self.phase_cycles[3] if self.phase_cycles[3] else None)
                                      for q, k in enumerate(("regen", "trace", "shade"))},
-                                    sample=(self.sample_cycles / self.phase_cycles[3] if self.phase_cycles[3] else None))}
+                                    **{k: (self.sub_cycles[q] / self.phase_cycles[3] if self.phase_cycles[3] else None)
+                                       for q, k in enumerate(("sample", "node_loop", "leaf_tests", "path_start"))})}
 
 
 class rtw_pixel(C.Structure):  # lib.rs:120-126 Pixel

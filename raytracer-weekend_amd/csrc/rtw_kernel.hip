@@ -469,7 +469,16 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint64_t seg,
-                          unsigned long long* err) {
+                          unsigned long long* err, uint64_t* tph) {
+  // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
+  uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+  auto tick = [&](int k) {
+    if (COUNT) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      tph[k] += t - tm;
+      tm = t;
+    }
+  };
   auto safe_inv = [](float d) {
     float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
     return __builtin_amdgcn_rcpf(dd);
@@ -569,12 +578,14 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       }
     }
     if (g2 == GUARD) break;
+    tick(0);
     if (ts.pend != 0) {  // phase 2
       const uint32_t v = ~(uint32_t)ts.pend;
       const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg);
       ts.pend = 0;
     }
+    tick(1);
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
     if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) return;
   }
@@ -869,8 +880,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   st.pid = 0;
   st.rng = 0;
   st.depth = 0;
-  uint64_t ph[4] = {0, 0, 0, 0};  // COUNT: wave-cycles in regeneration / traversal / shading / shading's
-                                 // rejection sampling
+  // COUNT: wave-cycles in regeneration / traversal / shading, then the sub-phases: shading's
+  // rejection sampling, traversal's node loop and leaf tests, regeneration's start_path
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
   const uint64_t t_start = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_mark = t_start;
   auto phase = [&](int k) {
@@ -903,10 +915,12 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
           exhausted = true;
         }
       }
+      const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
         if ((rank < avail || id < ne) && start_path(a, id, st)) has = true;
       }
+      if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
         pool_next += n_need;
       } else {
@@ -930,7 +944,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (!(FEAT & F_LIST)) {
       const uint32_t quota = ((uint32_t)__popcll(__ballot(1)) * a.quota16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, st.rng,
-                                           a.counters + 30);
+                                           a.counters + 30, ph + 4);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1011,7 +1025,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (lane == 0) {
       for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
       atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
-      atomicAdd(a.counters + 20, (unsigned long long)ph[3]);
+      for (int k = 3; k < 7; ++k) atomicAdd(a.counters + 17 + k, (unsigned long long)ph[k]);
     }
     for (int q = 0; q < 15; ++q) {
       unsigned long long c = cnt[q];
@@ -1381,7 +1395,7 @@ int collect_stats(DeviceCopy& c, void* stream_, void* ev0_, void* ev1_, uint64_t
   for (int k = 0; k < 6; ++k) st->simd[k] = cnt[9 + k];
   for (int k = 0; k < 4; ++k) st->phase_cycles[k] = cnt[16 + k];
   st->boxes_tested = cnt[15];
-  st->sample_cycles = cnt[20];
+  for (int k = 0; k < 4; ++k) st->sub_cycles[k] = cnt[20 + k];
   return RTW_OK;
 }
 

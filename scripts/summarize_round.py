@@ -1,0 +1,84 @@
+"""Turn a scripts/gpu_r02.sh run into the committed evidence under profiles/<round>/.
+
+    python scripts/summarize_round.py gpurun_out r02e_ profiles/r02 [configs...]
+
+Per config it copies the rocprofv3 kernel stats and PMC / SQ counter CSVs and the bench line
+(bench.json), writes profiles/pmc_<cfg>.json (HBM bytes per path-kernel launch: FETCH_SIZE x2 +
+WRITE_SIZE, KiB -> B, MI355X_MICROARCH.md §HBM) and profiles/valu_<cfg>.json (VALU busy, lane
+utilisation, waits; see scripts/valu_summary.py for the formulas), then prints scripts/roofline.py's
+recomputation of the roofline from those files.
+"""
+import csv
+import json
+import shutil
+import subprocess
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def per_dispatch(path, name_key="Kernel_Name", match="path_kernel<false"):
+    per = defaultdict(lambda: defaultdict(float))
+    kernel = None
+    for r in csv.DictReader(open(path)):
+        if match not in r[name_key]:
+            continue
+        d = r.get("Dispatch_Id") or r.get("Correlation_Id") or "0"
+        per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+        kernel = r[name_key]
+    out = defaultdict(float)
+    for cs in per.values():
+        for c, v in cs.items():
+            out[c] += v / len(per)
+    return dict(out), kernel, len(per)
+
+
+def main():
+    src, tag, dst = Path(sys.argv[1]), sys.argv[2], Path(sys.argv[3])
+    cfgs = sys.argv[4:] or ["jumpy-1080p", "cornell-800", "cow-1080p", "monument-4k"]
+    for cfg in cfgs:
+        s = src / f"{tag}{cfg}"
+        d = dst / cfg
+        d.mkdir(parents=True, exist_ok=True)
+        lines = [l for l in (s / "bench.log").read_text().splitlines() if l.startswith("{")]
+        (d / "bench.json").write_text(lines[-1] + "\n")
+        shutil.copy(s / "kt" / "kt_kernel_stats.csv", d / "kernel_stats.csv")
+        pmc = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            f = s / f"pmc_{c}" / "pmc_counter_collection.csv"
+            shutil.copy(f, d / f"pmc_{c.lower()}.csv")
+            v, kernel, n = per_dispatch(f)
+            pmc[c] = v[c] * 1024  # KiB -> B per launch
+        pub = {"config": cfg, "world": 1, "launches_per_frame": 1, "kernel": kernel,
+               "hbm_bytes_per_launch": 2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"],
+               "fetch_bytes_per_launch_raw": pmc["FETCH_SIZE"], "write_bytes_per_launch": pmc["WRITE_SIZE"],
+               "correction": "FETCH_SIZE x2 (gfx950 counts 64 B per 128-B request), WRITE_SIZE as is; KiB -> B",
+               "source": str(d.relative_to(ROOT))}
+        (ROOT / "profiles" / f"pmc_{cfg}.json").write_text(json.dumps(pub, indent=1))
+        c = {}
+        for i in (1, 2):
+            f = s / f"sq{i}" / "sq_counter_collection.csv"
+            shutil.copy(f, d / f"sq{i}_counter_collection.csv")
+            v, kernel, n = per_dispatch(f)
+            c.update(v)
+
+        def ratio(a, b, k=1.0):
+            return round(c[a] * k / c[b], 4) if a in c and c.get(b) else None
+
+        valu = {"config": cfg, "kernel": kernel, "dispatches": n,
+                "valu_busy": round(c["SQ_INSTS_VALU"] * 2 / (1024 * c["GRBM_GUI_ACTIVE"] / 8), 4),
+                "valu_lane_util": ratio("SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", 1 / 64),
+                "wave_wait": ratio("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"),
+                "wave_issue": ratio("SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"),
+                "l2_hit": round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4),
+                "counters": {k: round(v) for k, v in sorted(c.items())},
+                "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r02.sh)"}
+        (ROOT / "profiles" / f"valu_{cfg}.json").write_text(json.dumps(valu, indent=1))
+        print(cfg, "pmc", pub["hbm_bytes_per_launch"], "valu_busy", valu["valu_busy"], "lane", valu["valu_lane_util"])
+    subprocess.run([sys.executable, str(ROOT / "scripts" / "roofline.py"), str(dst)] + cfgs, check=True)
+
+
+if __name__ == "__main__":
+    main()
