@@ -53,6 +53,7 @@ def lib() -> C.CDLL:
                                         C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_int, _U32,
                                         C.c_uint32, _F, C.POINTER(C.c_uint64)]),
             "oracle_pcg32_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
+            "oracle_rng_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
             "oracle_splitmix64": (C.c_uint64, [C.c_uint64]),
             "oracle_path_state": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]),
             "oracle_u32_to_f32": (C.c_float, [C.c_uint32]),

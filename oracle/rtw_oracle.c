@@ -17,9 +17,10 @@
  *
  * RNG: the reference's rand 0.9.0-alpha.1 (Cargo.lock:2662-2670, not vendored) is
  * restated only for its float conversions (Standard f32/f64, UniformFloat
- * sample_single).  The bit source is this build's own PCG32 (XSH-RR 64/32) keyed
- * by (seed, pixel, sample) — the reference's ThreadRng is OS-seeded, so no bit
- * stream of it can be matched anyway.
+ * sample_single).  The bit source of a path is this build's xoroshiro64* (Blackman &
+ * Vigna 2018) seeded with splitmix64(splitmix64(seed) ^ (j << 48 | i << 32 | sample)) —
+ * the reference's ThreadRng is OS-seeded, so no bit stream of it can be matched anyway.
+ * Scene placement and the reference-BvhNode axis draws use a PCG32 (XSH-RR 64/32) stream.
  */
 #include "rtw_oracle.h"
 
@@ -77,6 +78,7 @@ uint64_t oracle_splitmix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+/* PCG32 (XSH-RR 64/32): the scene-placement / reference-BVH stream (host side only) */
 typedef struct { uint64_t s; } pcg32;
 static inline uint32_t pcg_next(pcg32* r) {
   uint64_t old = r->s;
@@ -91,10 +93,31 @@ uint32_t oracle_pcg32_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t
   if (state_out) *state_out = r.s;
   return n;
 }
-/* Per-path stream key: (seed, pixel row j, column i, sample s). */
+/* xoroshiro64* (Blackman & Vigna 2018): the per-path stream.  State = s0 | s1 << 32, never 0.
+ * One 32-bit multiply per draw (the GPU's PCG32 needed a 64-bit one); the multiply's high bits,
+ * which every float conversion below uses, pass BigCrush. */
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+static inline uint32_t xoro_next(uint64_t* st) {
+  uint32_t s0 = (uint32_t)*st, s1 = (uint32_t)(*st >> 32);
+  const uint32_t result = s0 * 0x9E3779BBu;
+  s1 ^= s0;
+  s0 = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
+  s1 = rotl32(s1, 13);
+  *st = ((uint64_t)s1 << 32) | s0;
+  return result;
+}
+/* seeds a stream from a 64-bit hash (the all-zero state is xoroshiro's fixed point) */
+static inline uint64_t xoro_seed(uint64_t h) { return h ? h : 0x9E3779B97F4A7C15ull; }
+uint32_t oracle_rng_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t* state_out) {
+  uint64_t st = state;
+  for (uint32_t k = 0; k < n; ++k) out[k] = xoro_next(&st);
+  if (state_out) *state_out = st;
+  return n;
+}
+/* Per-path stream state: (seed, pixel row j, column i, sample s); j, i < 2^16. */
 uint64_t oracle_path_state(uint64_t seed, uint32_t j, uint32_t i, uint32_t s) {
-  uint64_t h = oracle_splitmix64(oracle_splitmix64(seed) ^ (((uint64_t)j << 32) | i));
-  return oracle_splitmix64(h ^ (uint64_t)s);
+  const uint64_t key = ((uint64_t)j << 48) | ((uint64_t)i << 32) | (uint64_t)s;
+  return xoro_seed(oracle_splitmix64(oracle_splitmix64(seed) ^ key));
 }
 static inline float bits_to_f(uint32_t b) { float f; memcpy(&f, &b, 4); return f; }
 static inline uint32_t f_to_bits(float f) { uint32_t b; memcpy(&b, &f, 4); return b; }
@@ -111,16 +134,16 @@ static inline float range_attempt(uint32_t u, float scale, float lo) {
 }
 float oracle_u32_to_range(uint32_t u, float lo, float hi) { return range_attempt(u, hi - lo, lo); }
 
-/* A draw source: either a live PCG stream or an explicit array (unit tests). */
+/* A draw source: either a live path stream (xoroshiro64* state) or an explicit array (unit tests). */
 typedef struct {
-  pcg32 rng;
+  struct { uint64_t s; } rng;
   const uint32_t* arr;
   uint32_t n, used;
 } draws;
 static inline uint32_t next_u32(draws* d) {
   if (d->arr) { uint32_t v = d->used < d->n ? d->arr[d->used] : 0x80000000u; d->used++; return v; }  /* exhausted -> 0.0 in [-1,1) */
   d->used++;
-  return pcg_next(&d->rng);
+  return xoro_next(&d->rng.s);
 }
 static inline float gen_f32(draws* d) { return oracle_u32_to_f32(next_u32(d)); }
 static inline float gen_range(draws* d, float lo, float hi) {
@@ -549,8 +572,8 @@ static int node_hit(const onode* nd, const ray* r, float tmin, float tmax, int b
       t1 = fmaxf(t1, 0.0f);
       float len = sqrtf(vlen2(r->d)); /* vec3.rs:81-83 */
       float dist = (t2 - t1) * len;
-      pcg32 g = {oracle_splitmix64(g_seg ^ oracle_splitmix64((uint64_t)nd->key))};
-      float hd = nd->f[1] * oracle_log10f(oracle_u32_to_f32(pcg_next(&g)));
+      uint64_t g = xoro_seed(oracle_splitmix64(g_seg ^ oracle_splitmix64((uint64_t)nd->key)));
+      float hd = nd->f[1] * oracle_log10f(oracle_u32_to_f32(xoro_next(&g)));
       if (hd > dist) return 0;
       float t = t1 + hd / len;
       if (t > tmax) return 0;
@@ -941,6 +964,7 @@ int oracle_render(oracle_scene* s, const oracle_camera* cam, const float backgro
                   int bvh_mode, int n_threads, const uint32_t* rows, uint32_t n_rows, float* out,
                   uint64_t* rays) {
   if (!s || !cam || !out || w < 2 || h < 2) { set_err("bad arguments"); return -22; }
+  if (w > 65536 || h > 65536) { set_err("w, h <= 65536 (16-bit pixel coordinates in the path key)"); return -22; }
   job_t jb;
   memset(&jb, 0, sizeof jb);
   jb.s = s; jb.cam = cam; jb.bg = v3(background[0], background[1], background[2]);

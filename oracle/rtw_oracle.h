@@ -59,6 +59,7 @@ int oracle_render(oracle_scene* s, const oracle_camera* cam, const float backgro
 
 /* ---- unit-level entry points used by the KAT / golden-vector tests ---- */
 uint32_t oracle_pcg32_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t* state_out);
+uint32_t oracle_rng_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t* state_out);
 uint64_t oracle_splitmix64(uint64_t z);
 uint64_t oracle_path_state(uint64_t seed, uint32_t j, uint32_t i, uint32_t s);
 float oracle_u32_to_f32(uint32_t u);                       /* rand Standard f32 */

@@ -70,38 +70,45 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                 
 }
 __device__ __forceinline__ V3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 
-// ---- RNG: PCG32 XSH-RR keyed by (seed, pixel, sample); rand 0.9 float conversions
+// ---- RNG: xoroshiro64* per path (state s0 | s1 << 32, never 0) seeded by
+// splitmix64(splitmix64(seed) ^ (j << 48 | i << 32 | sample)); rand 0.9 float conversions
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
-  uint64_t old = s;
-  s = old * 6364136223846793005ull + 1442695040888963407ull;
-  uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-  uint32_t rot = (uint32_t)(old >> 59);
-  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+__device__ __forceinline__ uint64_t xoro_seed(uint64_t h) { return h ? h : 0x9E3779B97F4A7C15ull; }
+// one 32-bit multiply + 5 shift/rotate/xor ops per draw (the round-1 PCG32 step was a 64-bit
+// multiply: 3 quarter-rate VALU ops)
+__device__ __forceinline__ uint32_t rng_next(uint64_t& s) {
+  uint32_t s0 = (uint32_t)s, s1 = (uint32_t)(s >> 32);
+  const uint32_t result = s0 * 0x9E3779BBu;
+  s1 ^= s0;
+  s0 = __builtin_amdgcn_alignbit(s0, s0, 6) ^ s1 ^ (s1 << 9);  // rotl(s0, 26)
+  s1 = __builtin_amdgcn_alignbit(s1, s1, 19);                   // rotl(s1, 13)
+  s = ((uint64_t)s1 << 32) | s0;
+  return result;
 }
 __device__ __forceinline__ float gen_f32(uint64_t& s) {  // rand Standard<f32>
-  return (float)(pcg_next(s) >> 8) * (1.0f / 16777216.0f);
+  return (float)(rng_next(s) >> 8) * (1.0f / 16777216.0f);
 }
 __device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi, float sc) {
   // UniformFloat::sample_single with sc = hi - lo precomputed (kernel-uniform: stays in an SGPR)
   for (;;) {
-    float v01 = __uint_as_float((pcg_next(s) >> 9) | 0x3F800000u) - 1.0f;
+    float v01 = __uint_as_float((rng_next(s) >> 9) | 0x3F800000u) - 1.0f;
     float r = v01 * sc + lo;
     if (r < hi) return r;
     sc = __uint_as_float(__float_as_uint(sc) - 1u);
   }
 }
-// gen_range(s, -1, 1) without the retry loop: v01 = m * 2^-23 (m < 2^23), so v01 * 2 - 1 =
-// (m - 2^22) * 2^-22 is exact and at most 1 - 2^-22 < 1; the retry never fires (checked for
-// every m in tests/test_oracle_kat.py::test_pm1_never_retries).
+// gen_range(s, -1, 1) without the retry loop: v12 = 1 + m 2^-23 (m < 2^23), and
+// (v12 - 1) * 2 + -1 = 2 v12 - 3 = (m - 2^22) 2^-22 is exact in both forms and at most 1 - 2^-22 < 1,
+// so the retry never fires (checked for every m in tests/test_oracle_kat.py::test_pm1_never_retries)
+// and one exact fma gives the oracle's bits.
 __device__ __forceinline__ float gen_pm1(uint64_t& s) {
-  const float v01 = __uint_as_float((pcg_next(s) >> 9) | 0x3F800000u) - 1.0f;
-  return v01 * 2.0f + -1.0f;
+  const float v12 = __uint_as_float((rng_next(s) >> 9) | 0x3F800000u);
+  return __builtin_fmaf(v12, 2.0f, -3.0f);
 }
 __device__ __forceinline__ V3 rand_in_unit_sphere(uint64_t& s) {  // vec3.rs:101-108
   for (;;) {
@@ -356,7 +363,7 @@ __device__ __forceinline__ float cand_medium(const DevScene& S, const Ray& lr, c
   t1 = fmaxf(t1, 0.0f);
   const float len = sqrtf(len2(lr.d));
   const float dist = (r2 - t1) * len;
-  uint64_t g = splitmix64(seg ^ splitmix64((uint64_t)key));
+  uint64_t g = xoro_seed(splitmix64(seg ^ splitmix64((uint64_t)key)));
   const float hd = q2v.x * dev_log10f(gen_f32(g));
   if (hd > dist) return -1.0f;
   return t1 + hd / len;
@@ -839,7 +846,7 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   if (i >= a.w || row >= a.h) return false;
   const uint32_t j = a.h - 1u - row;
   const DevCamera& C = a.cam;
-  uint64_t rng = splitmix64(splitmix64(a.seed_hash ^ (((uint64_t)j << 32) | i)) ^ (uint64_t)s);
+  uint64_t rng = xoro_seed(splitmix64(a.seed_hash ^ (((uint64_t)j << 48) | ((uint64_t)i << 32) | s)));
   // lib.rs:84-86 + camera.rs:66-74
   const float u = ((float)i + gen_f32(rng)) / a.fw1;
   const float v = ((float)j + gen_f32(rng)) / a.fh1;
@@ -1279,6 +1286,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
                    float* d_out, void* stream_, uint32_t flags, void* ev0_, void* ev1_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   hipEvent_t ev0 = static_cast<hipEvent_t>(ev0_), ev1 = static_cast<hipEvent_t>(ev1_);
+  if (w > 65536u || h > 65536u)
+    return fail(RTW_EINVAL, "image %ux%u: at most 65536 x 65536 (16-bit pixel coordinates in the path key)", w, h);
   if (cam->time0 < sc.flat.time_lo || cam->time1 > sc.flat.time_hi)
     return fail(RTW_EINVAL, "camera shutter [%g, %g) outside the committed motion range [%g, %g]",
                 cam->time0, cam->time1, sc.flat.time_lo, sc.flat.time_hi);

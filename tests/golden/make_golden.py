@@ -56,6 +56,33 @@ class Pcg32:
         return ((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF
 
 
+class Xoro64:
+    """xoroshiro64* (Blackman & Vigna 2018): this build's per-path stream (DESIGN.md §Parity RNG)."""
+
+    def __init__(self, state: int):
+        self.s0, self.s1 = state & 0xFFFFFFFF, (state >> 32) & 0xFFFFFFFF
+
+    @staticmethod
+    def rotl(x, k):
+        return ((x << k) | (x >> (32 - k))) & 0xFFFFFFFF
+
+    def next_u32(self) -> int:
+        s0, s1 = self.s0, self.s1
+        result = (s0 * 0x9E3779BB) & 0xFFFFFFFF
+        s1 ^= s0
+        self.s0 = self.rotl(s0, 26) ^ s1 ^ ((s1 << 9) & 0xFFFFFFFF)
+        self.s1 = self.rotl(s1, 13)
+        return result
+
+    @property
+    def state(self) -> int:
+        return self.s0 | (self.s1 << 32)
+
+
+def xoro_seed(h: int) -> int:
+    return h if h else 0x9E3779B97F4A7C15
+
+
 class Draws:
     """Explicit u32 stream (unit vectors) with rand 0.9's float conversions."""
 
@@ -65,7 +92,7 @@ class Draws:
 
     def u32(self) -> int:
         self.used += 1
-        if isinstance(self.src, Pcg32):
+        if isinstance(self.src, (Pcg32, Xoro64)):
             return self.src.next_u32()
         return int(self.src[self.used - 1]) if self.used - 1 < len(self.src) else 0x80000000
 
@@ -86,8 +113,7 @@ class Draws:
 
 
 def path_state(seed, j, i, s):
-    h = splitmix64(splitmix64(seed) ^ ((j << 32) | i))
-    return splitmix64(h ^ s)
+    return xoro_seed(splitmix64(splitmix64(seed) ^ ((j << 48) | (i << 32) | s)))
 
 
 # ------------------------------------------------------------------ vec3.rs
@@ -339,7 +365,7 @@ def render_jumpy(w, h, spp, scene_seed, seed, aspect):
         for i in range(w):
             tot = v(0, 0, 0)
             for s in range(spp):
-                d = Draws(Pcg32(path_state(seed, j, i, s)))
+                d = Draws(Xoro64(path_state(seed, j, i, s)))
                 uu = F(F(F(i) + d.gen_f32()) / F(w - 1))
                 vv = F(F(F(j) + d.gen_f32()) / F(h - 1))
                 o, dirn, time = get_ray(cam, uu, vv, d)
@@ -467,7 +493,7 @@ def medium_hit(kind, par, o, d, tmin, tmax, density, seg, key):
     t1 = F(max(t1, F(0.0)))
     ln = F(np.sqrt(len2(d)))
     dist = F(F(r2 - t1) * ln)
-    u = Pcg32(splitmix64(seg ^ splitmix64(key))).next_u32()
+    u = Xoro64(xoro_seed(splitmix64(seg ^ splitmix64(key)))).next_u32()
     hd = F(neg_inv * log10f(F(u >> 8) * F(1.0 / 16777216.0)))
     if hd > dist:
         return None
@@ -486,6 +512,12 @@ def main():
         p = Pcg32(int(s))
         streams.append([p.next_u32() for _ in range(8)])
     g["pcg_stream"] = np.array(streams, np.uint32)
+    g["xoro_state"] = np.array([0x853C49E6748FEA9B, 1, 2 ** 63 + 7, 0xFFFFFFFF00000000], np.uint64)
+    xs = []
+    for st in g["xoro_state"]:
+        x = Xoro64(int(st))
+        xs.append([x.next_u32() for _ in range(8)])
+    g["xoro_stream"] = np.array(xs, np.uint32)
     keys = np.array([[0, 0, 0, 0], [7, 3, 5, 1], [2024, 1079, 1919, 511], [2 ** 40 + 3, 17, 9, 100]], np.uint64)
     g["path_keys"] = keys
     g["path_state"] = np.array([path_state(int(a), int(b), int(c), int(d)) for a, b, c, d in keys], np.uint64)

@@ -16,13 +16,24 @@ def bits(a):
     return np.asarray(a, np.float32).view(np.uint32)
 
 
-def test_pcg32_and_path_keys(orc):
+def test_rng_streams_and_path_keys(orc):
+    """The scene stream (PCG32), the per-path stream (xoroshiro64*) and the path keys."""
     L = orc.lib()
     for s, first, stream in zip(G["pcg_state"], G["pcg_out"], G["pcg_stream"]):
         out = (C.c_uint32 * 8)()
         L.oracle_pcg32_stream(int(s), 8, out, None)
         assert list(out) == [int(x) for x in stream]
         assert int(first[0]) == int(stream[0])
+    for s, stream in zip(G["xoro_state"], G["xoro_stream"]):
+        out = (C.c_uint32 * 8)()
+        L.oracle_rng_stream(int(s), 8, out, None)
+        assert list(out) == [int(x) for x in stream]
+    # xoroshiro64*'s published first outputs for the state s0 = 1, s1 = 0: 0x9E3779BB, then
+    # s0' = rotl(1, 26) ^ 1 ^ (1 << 9) -> result s0' * 0x9E3779BB
+    out = (C.c_uint32 * 2)()
+    L.oracle_rng_stream(1, 2, out, None)
+    s0 = ((1 << 26) ^ 1 ^ (1 << 9)) & 0xFFFFFFFF
+    assert list(out) == [0x9E3779BB, (s0 * 0x9E3779BB) & 0xFFFFFFFF]
     for key, want in zip(G["path_keys"], G["path_state"]):
         assert L.oracle_path_state(*[int(k) for k in key]) == int(want)
 
