@@ -28,7 +28,8 @@ enum PrimType : uint32_t {
 
 struct alignas(16) DevPrim {
   // sphere : q0 = (cx, cy, cz, r)
-  // msphere: q0 = (c0x, c0y, c0z, t0), q1 = (c1x, c1y, c1z, t1), q2.x = r
+  // msphere: q0 = (c0x, c0y, c0z, r*r), q1 = (c1-c0 xyz, r), q2 = (t0, t1, -, -), aux = 1 if the
+  //          shutter is [+0, 1] (center_at then needs no division and no q2)
   // rect   : q0 = (a0, a1, b0, b1), q1.x = k
   // tri    : q0 = (ax, ay, az, abx), q1 = (aby, abz, acx, acy), q2 = (acz, nx, ny, nz)
   //          ab = b - a, ac = c - a, n = ab x ac (bit-identical to triangular.rs:101-105)
@@ -38,7 +39,7 @@ struct alignas(16) DevPrim {
   uint32_t type_inst;  // bits 0..7 PrimType, bits 8..31 instance id (0 = identity)
   uint32_t key;        // global DFS leaf index: the tie-break (later object wins, mod.rs:61-65)
   uint32_t mat;        // material id
-  uint32_t aux;        // triangle: index into tshade; medium: inner (boundary) instance id
+  uint32_t aux;        // triangle: index into tshade; medium: inner (boundary) instance id; msphere: unit shutter
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
 
@@ -159,6 +160,9 @@ struct DevScene {
   const DevPerlin* perlins;
   const DevShade* shade;
   uint32_t n_nodes, n_prims, n_always, n_insts;
+  uint32_t msphere_unit;  // every moving sphere's shutter is [+0, 1]: center_at needs no q2 / division
+  uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
+  float uni_off[3];
 };
 
 struct DevCamera {

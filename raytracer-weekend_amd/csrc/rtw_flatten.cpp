@@ -181,13 +181,19 @@ struct Builder {
         DevPrim p;
         memset(&p, 0, sizeof p);
         p.type_inst = PT_MSPHERE;
-        // q0 = (c0, t0), q1 = (c1 - c0, t1), q2 = (r, r * r): the f32 subtraction and product the
-        // reference evaluates per call (spherical.rs:29, :117-123), done once here (same IEEE ops)
-        memcpy(p.q0, n.f, 4 * sizeof(float));
+        // q0 = (c0, r * r), q1 = (c1 - c0, r), q2 = (t0, t1): the f32 subtraction and product the
+        // reference evaluates per call (spherical.rs:29, :117-123), done once here (same IEEE ops).
+        // aux = 1 for the shutter [+0, 1], where (time - t0) / (t1 - t0) is `time` exactly; when every
+        // moving sphere has it (Flat::msphere_unit) the test needs q0, q1 and meta only (one round trip)
+        memcpy(p.q0, n.f, 3 * sizeof(float));
+        p.q0[3] = n.f[8] * n.f[8];
         for (int a = 0; a < 3; ++a) p.q1[a] = n.f[4 + a] - n.f[a];
-        p.q1[3] = n.f[7];
-        p.q2[0] = n.f[8];
-        p.q2[1] = n.f[8] * n.f[8];
+        p.q1[3] = n.f[8];
+        p.q2[0] = n.f[3];
+        p.q2[1] = n.f[7];
+        uint32_t t0_bits;
+        memcpy(&t0_bits, &n.f[3], 4);
+        p.aux = (t0_bits == 0u && n.f[7] == 1.0f) ? 1u : 0u;
         p.mat = n.mat;
         float r = fabsf(n.f[8]);
         Box b;
@@ -644,6 +650,16 @@ int flatten(Scene& s) {
   }
   // feature set (selects the specialised kernel)
   uint32_t F = 0;
+  // one translate-only wrapper for every instanced prim (cow, monument: the mesh under one
+  // Translation): the kernel subtracts its kernel-uniform offset instead of loading the chain
+  f.uni_inst = 0;
+  if (f.insts.size() == 2 && f.insts[1].nops == 1 && f.insts[1].op[0][0] == (float)IO_TRANSLATE) {
+    f.uni_inst = 1;
+    for (int a = 0; a < 3; ++a) f.uni_off[a] = f.insts[1].op[0][1 + a];
+  }
+  f.msphere_unit = 1;
+  for (const DevPrim& p : f.prims)
+    if ((p.type_inst & 0xffu) == PT_MSPHERE && !p.aux) f.msphere_unit = 0;
   for (const DevPrim& p : f.prims) {
     const uint32_t t = p.type_inst & 0xffu;
     F |= t == PT_SPHERE ? F_SPHERE : t == PT_MSPHERE ? F_MSPHERE : t == PT_TRI ? F_TRI : t == PT_MEDIUM ? F_MEDIUM : F_RECT;

@@ -253,13 +253,17 @@ __device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad2) {  
   if (root < TMIN) root = (-hb + sq) / a;  // root1 > t_max implies root2 > t_max
   return root;
 }
-// spherical.rs:117-123 over the flattened layout q0 = (c0, t0), q1 = (c1 - c0, t1) (rtw_flatten.cpp).
-// For the shutter [+0, 1] the fraction (time - 0) / (1 - 0) is `time` exactly: the IEEE division
-// is skipped (a wave-uniform branch in practice: every moving sphere of a scene shares it).
-__device__ __forceinline__ V3 center_at(const float* q0, const float* q1, float time) {
+// spherical.rs:117-123 over the flattened layout q0 = (c0, r*r), q1 = (c1 - c0, r), q2 = (t0, t1)
+// (rtw_flatten.cpp).  For the shutter [+0, 1] (aux = 1) the fraction (time - 0) / (1 - 0) is `time`
+// exactly: when every moving sphere of the scene has it (DevScene::msphere_unit, a kernel-uniform
+// branch) the IEEE division and the q2 load are skipped; otherwise each prim's t0, t1 are used.
+__device__ __forceinline__ V3 center_at(float4 q0, float4 q1, const float4* P, uint32_t unit_shutter, float time) {
   float frac = time;
-  if (__float_as_uint(q0[3]) != 0u || q1[3] != 1.0f) frac = (time - q0[3]) / (q1[3] - q0[3]);
-  return add(ld3(q0), scale(ld3(q1), frac));
+  if (!unit_shutter) {
+    const float4 q2 = P[2];
+    frac = (time - q2.x) / (q2.y - q2.x);
+  }
+  return add(mk(q0.x, q0.y, q0.z), scale(mk(q1.x, q1.y, q1.z), frac));
 }
 template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
 __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float k) {
@@ -384,28 +388,36 @@ template <bool COUNT, uint32_t FEAT, bool LOCAL = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
                                           uint32_t* cnt, uint64_t seg) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
+  // every 16-B part the scene's primitive kinds may need is loaded up front, in one round trip:
+  // loading the geometry only after the type was known cost two more dependent trips per test
   const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
   const float4 q0v = P[0];
+  constexpr bool NEED_Q1 = (FEAT & (F_MSPHERE | F_TRI | F_RECT)) != 0, NEED_Q2 = (FEAT & F_TRI) != 0;
+  const float4 q1v = NEED_Q1 ? P[1] : q0v;
+  const float4 q2v = NEED_Q2 ? P[2] : q0v;
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
   // object-space ray of the prim's wrapper chain; in BVH leaves recomputed per test (a few
   // flops) rather than cached, which keeps 8 VGPRs free for occupancy
-  const Ray lr = (!LOCAL && (FEAT & F_INST) && inst) ? to_local(S.insts + inst, wr) : wr;
+  Ray lr = wr;
+  if (!LOCAL && (FEAT & F_INST) && inst) {
+    if (inst == S.uni_inst)  // transformations.rs:23-38 with the kernel-uniform offset: no dependent loads
+      lr.o = sub(wr.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
+    else
+      lr = to_local(S.insts + inst, wr);
+  }
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
   float t = -1.0f;
   if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
     t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3] * q0[3]);
   } else if ((FEAT & F_MSPHERE) && type == PT_MSPHERE) {
-    const float4 q1v = P[1];
-    const float q1[4] = {q1v.x, q1v.y, q1v.z, q1v.w};
-    t = cand_sphere(lr, center_at(q0, q1, lr.time), P[2].y);
+    t = cand_sphere(lr, center_at(q0v, q1v, P, S.msphere_unit, lr.time), q0v.w);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
-    const float4 q1v = P[1], q2v = P[2];
     const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
     t = cand_tri(lr, q);
   } else if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {
     t = cand_medium<FEAT>(S, lr, P, meta.y, meta.w, seg);
   } else if (FEAT & F_RECT) {
-    const float k = P[1].x;
+    const float k = q1v.x;
     if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
     else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
     else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
@@ -630,8 +642,10 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   V3 outward;
   h.p = add(lr.o, scale(lr.d, t));  // ray.rs:25-27
   if (((FEAT & F_SPHERE) && type == PT_SPHERE) || ((FEAT & F_MSPHERE) && type == PT_MSPHERE)) {
-    V3 c = type == PT_SPHERE ? ld3(P.q0) : center_at(P.q0, P.q1, lr.time);
-    float rad = type == PT_SPHERE ? P.q0[3] : P.q2[0];
+    const float4* PP = reinterpret_cast<const float4*>(S.prims + b.prim);
+    const float4 q0 = PP[0], q1 = PP[1];
+    V3 c = type == PT_SPHERE ? mk(q0.x, q0.y, q0.z) : center_at(q0, q1, PP, S.msphere_unit, lr.time);
+    float rad = type == PT_SPHERE ? q0.w : q1.w;
     outward = divs(sub(h.p, c), rad);
     if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
@@ -1139,6 +1153,9 @@ int upload(Scene& s, int device) {
     c.scene.n_prims = (uint32_t)f.prims.size();
     c.scene.n_always = (uint32_t)f.always.size();
     c.scene.n_insts = (uint32_t)f.insts.size();
+    c.scene.msphere_unit = f.msphere_unit;
+    c.scene.uni_inst = f.uni_inst;
+    memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
     s.dev.push_back(c);
   }
   hipSetDevice(prev);

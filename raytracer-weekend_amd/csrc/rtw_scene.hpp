@@ -69,6 +69,9 @@ struct Flat {
   std::vector<DevPerlin> perlins;
   uint32_t depth = 0;
   uint32_t features = 0;  // Feature bits actually used
+  uint32_t msphere_unit = 1;  // every moving sphere has the shutter [+0, 1] (DevPrim::aux)
+  uint32_t uni_inst = 0;      // the only instance, a single Translation (0 = none such)
+  float uni_off[3] = {0, 0, 0};
   float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover
 };
 
