@@ -8,7 +8,7 @@
 //                         is a contiguous run; geometry in q0..q2, meta in the last 16 B.
 //   always  : uint32[]    primitives tested for every ray (huge boxes, e.g. the
 //                         r=1000 ground sphere) instead of polluting the BVH.
-//   tshade  : DevTriShade per triangle: vertex normals + uvs, read only for the winner.
+//   tshade  : DevTriShade per prim (triangles only filled): vertex normals + uvs, read only for the winner.
 //   insts   : DevInst[]   wrapper chains (Translation / YRotation), outer -> inner.
 //   mats, texs, texels   : material / texture tables and RGB8 image data.
 #pragma once
@@ -39,7 +39,7 @@ struct alignas(16) DevPrim {
   uint32_t type_inst;  // bits 0..7 PrimType, bits 8..31 instance id (0 = identity)
   uint32_t key;        // global DFS leaf index: the tie-break (later object wins, mod.rs:61-65)
   uint32_t mat;        // material id
-  uint32_t aux;        // triangle: index into tshade; medium: inner (boundary) instance id; msphere: unit shutter
+  uint32_t aux;        // triangle: index into tshade (= its prim index); medium: inner (boundary) instance id; msphere: unit shutter
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
 

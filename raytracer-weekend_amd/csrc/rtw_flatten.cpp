@@ -586,6 +586,18 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // triangle shading data re-indexed by prim (tshade[k] belongs to prims[k]): the winner's
+  // normals / uvs load straight from the hit's prim index, beside its geometry
+  if (!f.tshade.empty()) {
+    std::vector<DevTriShade> by_prim(f.prims.size());
+    memset(by_prim.data(), 0, by_prim.size() * sizeof(DevTriShade));
+    for (size_t k = 0; k < f.prims.size(); ++k)
+      if ((f.prims[k].type_inst & 0xffu) == PT_TRI) {
+        by_prim[k] = f.tshade[f.prims[k].aux];
+        f.prims[k].aux = (uint32_t)k;
+      }
+    f.tshade.swap(by_prim);
+  }
   // shading records (one per prim, same order)
   for (const DevPrim& p : f.prims) {
     const DevMat& m = f.mats[p.mat];

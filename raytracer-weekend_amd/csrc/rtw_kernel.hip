@@ -633,7 +633,10 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   const DevPrim P = S.prims[b.prim];
   const uint32_t type = P.type_inst & 0xffu, inst = P.type_inst >> 8;
   const DevInst* I = S.insts + inst;
-  const Ray lr = ((FEAT & F_INST) && inst) ? to_local(I, wr) : wr;
+  const bool uni = (FEAT & F_INST) && inst && inst == S.uni_inst;  // one Translation, offset uniform
+  Ray lr = wr;
+  if (uni) lr.o = sub(wr.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
+  else if ((FEAT & F_INST) && inst) lr = to_local(I, wr);
   const float t = b.t;
   Rec h;
   h.mat = P.mat;
@@ -652,7 +655,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
                          P.q1[2], P.q1[3], P.q2[0], P.q2[1], P.q2[2], P.q2[3]};
     TriUV s = tri_solve(lr, q);
-    const DevTriShade& sh = S.tshade[P.aux];
+    const DevTriShade& sh = S.tshade[b.prim];  // indexed like prims[] (rtw_flatten.cpp)
     float w = 1.0f - s.u - s.v;  // triangular.rs:315-323
     outward = add(add(scale(ld3(sh.n), w), scale(ld3(sh.n + 3), s.u)), scale(ld3(sh.n + 6), s.v));
     h.u = (w * sh.uv[0] + s.u * sh.uv[2]) + s.v * sh.uv[4];
@@ -673,7 +676,10 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   } else {
     face(h, lr.d, outward);
   }
-  if ((FEAT & F_INST) && inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
+  if (uni) {  // transformations.rs:29-37: p + offset, face normal against the world ray
+    h.p = add(h.p, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
+    face(h, wr.d, h.n);
+  } else if ((FEAT & F_INST) && inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
     for (int k = (int)I->nops - 1; k >= 0; --k) {
       V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
       for (int q = 0; q <= k; ++q) {
