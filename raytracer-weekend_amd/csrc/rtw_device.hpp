@@ -179,6 +179,7 @@ struct RenderArgs {
   uint32_t slot_base;         // first tile slot of this pass
   uint32_t quota16;           // trace_run returns once quota16/16 of the wave's lanes are done
   uint32_t regen_min;         // regenerate once this many lanes are idle (or every lane is)
+  uint32_t batch;             // path ids a wave takes from the global queue per atomic
   uint64_t spp_magic;         // UINT64_MAX / spp + 1 (dev::fastdiv; spp >= 2)
   float fw1, fh1;             // (float)(w - 1), (float)(h - 1) (lib.rs:84-85 divisors)
   float time_span;            // cam.time1 - cam.time0 in f32 (UniformFloat scale, camera.rs:72)

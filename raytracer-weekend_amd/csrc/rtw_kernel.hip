@@ -933,11 +933,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       if (avail < n_need) {  // refill: one atomic per BATCH paths
         // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)BATCH);
+        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)a.batch);
         const uint64_t b = rfl64(pool[2]);
         if (b < P) {
           nb = b;
-          ne = b + BATCH < P ? b + BATCH : P;
+          ne = b + a.batch < P ? b + a.batch : P;
         } else {
           exhausted = true;
         }
@@ -1338,6 +1338,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   }
   a.tiles_x_magic = a.tiles_x > 1u ? UINT64_MAX / a.tiles_x + 1u : 0u;
   a.tile_ids = d_tiles;
+  a.batch = (uint32_t)std::min(65536, std::max(64, env_int("RTW_BATCH", (int)dev::BATCH)));
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
   if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
   // the host mirror of dev::splitmix64 (seed pre-hash shared by every pixel)
