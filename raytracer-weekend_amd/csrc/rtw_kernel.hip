@@ -828,7 +828,11 @@ __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // 
 // grid drains with a one-path tail.  Each finished path writes L to the ordered sample
 // buffer (path-major RGB, 12 B per path in HBM); reduce_kernel then sums each pixel's samples in
 // sample order — exactly lib.rs:83-87's `pixel_color += sample_ray(..)` sequence.
-constexpr uint32_t BATCH = 256;
+// Path ids a wave takes per returning atomic on the one global queue word.  Every wave of the
+// grid hits that word: at 256 ids per atomic, short-path scenes spent most of their time behind it
+// (MI355X, RTW_BATCH sweep: cow-1080p 19.0k -> 30.1k Mrays/s, monument-4k 12.8k -> 17.0k, jumpy-1080p
+// 19.4k -> 20.4k at 2048); the tail this leaves is one batch per wave (~0.1 ms).  Knob RTW_BATCH.
+constexpr uint32_t BATCH = 2048;
 
 struct PathState {
   Ray ray;
