@@ -57,8 +57,8 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
 # FP32 flop model (BASELINE.md roofline; DESIGN.md §5 derives each constant)
 FLOP_BOX = 21              # aabb.rs:23-48: per axis 1 div + 2 sub + 2 mul + min + max
 FLOP_PRIM = [23, 35, 6, 6, 6, 51]  # sphere (spherical.rs:26-44), moving (+12, :117-123), rect xy/xz/yz, triangle
-FLOP_SEGMENT = 60          # hit record + scatter + throughput per world.hit query
-FLOP_PATH = 50             # Camera::get_ray + pixel u, v per path (camera.rs:66-74, lib.rs:84-85)
+FLOP_SEGMENT = 65          # hit record + Lambertian scatter + throughput per world.hit query
+FLOP_PATH = 59             # pixel u, v + Camera::get_ray per path (lib.rs:84-85, camera.rs:66-74)
 # cache-level algorithmic bytes (the round-1 figure; operands come from L1/L2, not HBM)
 RAY_STATE_B = 64
 NODE_BOX_B = 32

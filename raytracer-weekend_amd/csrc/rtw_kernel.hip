@@ -715,8 +715,8 @@ __device__ __forceinline__ bool checker_odd_slow(float fx, float fy, float fz) {
   const float f[3] = {fx, fy, fz};
   uint32_t neg = 0;
   float tiny = 1.0f;  // left-to-right product of the tiny factors (sinf x == x there)
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
+#pragma unroll 1
+  for (int k = 0; k < 3; ++k) {  // cold path: one copy of the reduction, not three
     const float x = f[k], ax = fabsf(x);
     if (x != x || isinf(x) || x == 0.0f) return false;  // NaN or +-0 product: `< 0` is false
     if (ax < 0x1p-12f) tiny = tiny * ax;
