@@ -16,8 +16,8 @@ lib.rs:102, counted exactly by the kernel) / max-over-ranks step time.
 
 `roofline`: the path kernel is bound by VALU issue (SQ counters), so the
 roofline is FP32 VALU: algorithmic flops per launch (SURVEY.md §8d / BASELINE.md: 21 per box
-tested, 23 per sphere test (+12 moving), 6 per rect, 51 per triangle, + the shading and camera
-constants below) / the kernel's average HIP-event duration, vs the 157.3 TFLOP/s FP32 vector
+tested, 23 per sphere test (+12 moving), 6 per rect, 51 per triangle, 70 per scattering segment,
+64 per path; DESIGN.md §5 itemises them) / the kernel's average HIP-event duration, vs the 157.3 TFLOP/s FP32 vector
 peak.  Reported beside it: the measured HBM fraction (rocprofv3 PMC bytes per launch / duration /
 8 TB/s), the SQ-counter VALU lane-capacity figure (VALU busy x lane utilisation) and the
 cache-level algorithmic bytes.  scripts/roofline.py recomputes all of them from profiles/.
@@ -57,8 +57,8 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
 # FP32 flop model (BASELINE.md roofline; DESIGN.md §5 derives each constant)
 FLOP_BOX = 21              # aabb.rs:23-48: per axis 1 div + 2 sub + 2 mul + min + max
 FLOP_PRIM = [23, 35, 6, 6, 6, 51]  # sphere (spherical.rs:26-44), moving (+12, :117-123), rect xy/xz/yz, triangle
-FLOP_SEGMENT = 65          # hit record + Lambertian scatter + throughput per world.hit query
-FLOP_PATH = 59             # pixel u, v + Camera::get_ray per path (lib.rs:84-85, camera.rs:66-74)
+FLOP_SCATTER = 70          # hit record + Lambertian scatter + throughput per scattering segment
+FLOP_PATH = 64             # pixel u, v + Camera::get_ray + the terminal T * colour, per path
 # cache-level algorithmic bytes (the round-1 figure; operands come from L1/L2, not HBM)
 RAY_STATE_B = 64
 NODE_BOX_B = 32
@@ -131,8 +131,9 @@ def cpu_baseline(scene, cam, bg, w, h, spp, budget_s: float) -> dict:
 
 def flops_model(counts: dict) -> float:
     """Algorithmic FP32 flops of the counted work."""
+    # every path's last segment ends it (miss, light, absorption, depth); the others scatter
     return (FLOP_BOX * counts["boxes"] + float(np.dot(counts["prims"], FLOP_PRIM))
-            + FLOP_SEGMENT * counts["rays"] + FLOP_PATH * counts["paths"])
+            + FLOP_SCATTER * max(0.0, counts["rays"] - counts["paths"]) + FLOP_PATH * counts["paths"])
 
 
 def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: int, traffic, issue) -> dict:

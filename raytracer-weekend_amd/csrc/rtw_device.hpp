@@ -107,7 +107,7 @@ enum ShadeMode : uint32_t {
 struct alignas(16) DevShade {
   uint32_t kind;  // bits 0..7 MatType, bits 8..11 ShadeMode, bit 12 the material reads uv
   float param;    // metal fuzz | dielectric ir | checker frequency (Lambertian / light / isotropic)
-  float a[3];
+  float a[3];     // colour | Metal albedo | Dielectric (1 / ir, r0 at ratio 1 / ir, r0 at ratio ir)
   float b[3];
 };
 static_assert(sizeof(DevShade) == 32, "DevShade must be 32 B");

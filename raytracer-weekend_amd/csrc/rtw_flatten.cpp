@@ -611,6 +611,16 @@ int flatten(Scene& s) {
     } else if (m.type == MT_DIELECTRIC) {
       mode = SM_SOLID;  // attenuation (1, 1, 1), no texture
       d.param = m.param;
+      // material.rs:120 (1.0 / ir) and :108-112 (Schlick r0) for both refraction ratios: the kernel's
+      // f32 operations, evaluated once here (IEEE f32 on the host as on the device)
+      const volatile float one = 1.0f;
+      auto r0 = [&](float ri) {
+        const float x = (one - ri) / (one + ri);
+        return x * x;
+      };
+      d.a[0] = one / m.param;
+      d.a[1] = r0(d.a[0]);
+      d.a[2] = r0(m.param);
     } else {  // Lambertian, DiffuseLight, Isotropic: a texture
       const DevTex& t = f.texs[m.tex];
       if (t.type == TT_SOLID) {

@@ -32,6 +32,10 @@
 namespace rtw {
 namespace dev {
 
+#ifndef RTW_DIEL_PRE
+#define RTW_DIEL_PRE 1  // Dielectric 1 / ir and r0 precomputed by the flattener (DevShade::a)
+#endif
+
 constexpr float TMIN = 0.001f;  // lib.rs:102
 constexpr int BLOCK = 256;
 // LDS traversal-stack entries per lane (+ 1 scratch row).  At the 5 waves/SIMD the default
@@ -83,7 +87,11 @@ __device__ __forceinline__ uint64_t xoro_seed(uint64_t h) { return h ? h : 0x9E3
 // multiply: 3 quarter-rate VALU ops)
 __device__ __forceinline__ uint32_t rng_next(uint64_t& s) {
   uint32_t s0 = (uint32_t)s, s1 = (uint32_t)(s >> 32);
+#if RTW_RNG_PLUS
+  const uint32_t result = s0 + s1;
+#else
   const uint32_t result = s0 * 0x9E3779BBu;
+#endif
   s1 ^= s0;
   s0 = __builtin_amdgcn_alignbit(s0, s0, 6) ^ s1 ^ (s1 << 9);  // rotl(s0, 26)
   s1 = __builtin_amdgcn_alignbit(s1, s1, 19);                   // rotl(s1, 13)
@@ -810,9 +818,11 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
   return mk(0.f, 0.f, 0.f);
 }
 
-__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // material.rs:108-112
-  float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
-  r0 = r0 * r0;
+__device__ __forceinline__ float schlick_r0(float ref_idx) {  // material.rs:109-110
+  const float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+  return r0 * r0;
+}
+__device__ __forceinline__ float reflectance(float cosine, float r0) {  // material.rs:108-112, r0 = schlick_r0
   float x = 1.0f - cosine;
   float x2 = x * x;
   return r0 + (1.0f - r0) * (x * (x2 * x2));  // powi(5) as LLVM expands it
@@ -1029,11 +1039,19 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
           dir = add(reflect(ud, h.n), scale(rs, sh.param));
           done = !(dot(dir, h.n) > 0.0f);  // absorbed: emitted() is black
         } else if (!iso && (FEAT & F_DIEL)) {  // Dielectric, material.rs:116-142
+#if RTW_DIEL_PRE
+          // 1 / ir (material.rs:120) and Schlick's r0 (:108-112) for both ratios: the same f32
+          // operations, evaluated once by the flattener (DevShade::a)
+          const float ratio = h.front ? sh.a[0] : sh.param;
+          const float r0 = h.front ? sh.a[1] : sh.a[2];
+#else
           const float ratio = h.front ? 1.0f / sh.param : sh.param;
+          const float r0 = schlick_r0(ratio);
+#endif
           const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
           const float sin_t = sqrtf(1.0f - cos_t * cos_t);
           const bool cannot = (ratio * sin_t) > 1.0f;
-          if (cannot || reflectance(cos_t, ratio) > gen_f32(st.rng)) dir = reflect(ud, h.n);
+          if (cannot || reflectance(cos_t, r0) > gen_f32(st.rng)) dir = reflect(ud, h.n);
           else dir = refract(ud, h.n, ratio);
         }
         st.T = mul(st.T, att);  // x * 1.0f == x: the Dielectric's T is unchanged

@@ -10,7 +10,8 @@ Per config it reads
   profiles/valu_<cfg>.json        SQ counters (VALU busy, lane utilisation)
 and prints, from the rocprof average duration of the path kernel:
   FP32-VALU frac  = algorithmic flops per launch (bench.flops_model: 21 / box tested, 23 / sphere,
-                    35 / moving sphere, 6 / rect, 51 / triangle, 65 / segment, 59 / path)
+                    35 / moving sphere, 6 / rect, 51 / triangle, 70 / scattering segment,
+                    64 / path)
                     / avg duration / 157.3 TFLOP/s
   HBM frac        = PMC bytes per launch / avg duration / 8 TB/s
   VALU lane frac  = VALU busy x lane utilisation (share of the SIMDs' lane-cycles doing VALU work)
