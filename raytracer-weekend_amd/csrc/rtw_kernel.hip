@@ -538,6 +538,16 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         ts.pend = popl ? top : ts.pend;
         ts.sp -= (popn || popl) ? 1 : 0;
       }
+#ifdef RTW_LANE_DIAG
+      if (COUNT) {  // lane states per node-loop iteration (diagnostic build): all, descending, parked, done
+        const uint64_t bd = __ballot(ts.node >= 0), bp = __ballot(ts.node < 0 && ts.pend != 0);
+        const uint64_t bn = __ballot(ts.node < 0 && ts.pend == 0 && ts.sp == 0);
+        tph[3] += 64;  // per lane (the wave-uniform values are added by every lane: ratios are unaffected)
+        tph[4] += (uint64_t)__popcll(bd);
+        tph[5] += (uint64_t)__popcll(bp);
+        tph[6] += (uint64_t)__popcll(bn);
+      }
+#endif
       if (!__any(ts.node >= 0 && ts.pend == 0)) break;
       if (ts.node >= 0) {
         const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
@@ -923,7 +933,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   st.depth = 0;
   // COUNT: wave-cycles in regeneration / traversal / shading, then the sub-phases: shading's
   // rejection sampling, traversal's node loop and leaf tests, regeneration's start_path
-  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [7..10]: RTW_LANE_DIAG builds only
   const uint64_t t_start = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_mark = t_start;
   auto phase = [&](int k) {
@@ -1074,7 +1084,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
     if (lane == 0) {
       for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
       atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
+#ifdef RTW_LANE_DIAG
+      for (int k = 7; k < 11; ++k) atomicAdd(a.counters + 13 + k, (unsigned long long)ph[k]);
+#else
       for (int k = 3; k < 7; ++k) atomicAdd(a.counters + 17 + k, (unsigned long long)ph[k]);
+#endif
     }
     for (int q = 0; q < 15; ++q) {
       unsigned long long c = cnt[q];
