@@ -146,7 +146,7 @@ def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: in
            "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
            "flops_per_launch": round(flops), "kernel_ms_per_launch": round(kernel_ms_per_launch, 3),
            "flops_per_ray": round(flops_model(counts) / max(1, counts["rays"]), 1),
-           "hbm": None, "valu_lane": None,
+           "hbm": None, "valu_lane": None, "vmem_units": None,
            "cache_level": {"alg_bytes_per_launch": round(alg_bytes),
                            "GBps": round(alg_bytes / (kernel_ms_per_launch * 1e-3) / 1e9, 1),
                            "note": "node/prim operands are L1/L2 hits; not an HBM figure"}}
@@ -158,6 +158,8 @@ def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: in
         out["valu_lane"] = {"valu_busy": issue["valu_busy"], "lane_util": issue["valu_lane_util"],
                             "frac": round(issue["valu_busy"] * issue["valu_lane_util"], 4),
                             "source": issue.get("source")}
+    if issue and issue.get("ta_busy"):  # vector-memory units (busy, but not the one binding limit)
+        out["vmem_units"] = {"ta_busy": issue["ta_busy"], "td_busy": issue.get("td_busy"), "source": issue.get("source")}
     return out
 
 
@@ -330,7 +332,8 @@ def main() -> int:
     vj = ROOT / "profiles" / f"valu_{args.config}.json"
     if vj.exists() and not args.spp:
         d = json.loads(vj.read_text())
-        issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit")}
+        issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit",
+                                        "ta_busy", "td_busy")}
         issue["source"] = str(vj.relative_to(ROOT))
     n_launch = launches * passes
     # per launch of this rank (multi-device: device 0's launches, its 1/N share of the frame)

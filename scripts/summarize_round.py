@@ -58,8 +58,10 @@ def main():
                "source": str(d.relative_to(ROOT))}
         (ROOT / "profiles" / f"pmc_{cfg}.json").write_text(json.dumps(pub, indent=1))
         c = {}
-        for i in (1, 2):
+        for i in (1, 2, 3):
             f = s / f"sq{i}" / "sq_counter_collection.csv"
+            if not f.exists():
+                continue
             shutil.copy(f, d / f"sq{i}_counter_collection.csv")
             v, kernel, n = per_dispatch(f)
             c.update(v)
@@ -73,6 +75,9 @@ def main():
                 "wave_wait": ratio("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"),
                 "wave_issue": ratio("SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"),
                 "l2_hit": round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4),
+                # TA / TD busy: cycles summed over the 256 CUs vs GRBM_GUI_ACTIVE summed over the 8 XCDs
+                "ta_busy": round(c["TA_TA_BUSY_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "TA_TA_BUSY_sum" in c else None,
+                "td_busy": round(c["TD_TD_BUSY_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "TD_TD_BUSY_sum" in c else None,
                 "counters": {k: round(v) for k, v in sorted(c.items())},
                 "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r02.sh)"}
         (ROOT / "profiles" / f"valu_{cfg}.json").write_text(json.dumps(valu, indent=1))
