@@ -499,6 +499,11 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
                           unsigned long long* err, uint64_t* tph) {
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+  // Waves walking the tree issue before waves shading or regenerating (the path kernel drops the
+  // priority again when trace_run returns).  MI355X A/B (profiles/r02/experiments, s1/s2): jumpy
+  // +1.7%, cow +1.6%, monument +0.7%; shading first, node-load issue first or graded levels were
+  // slower or equal.
+  __builtin_amdgcn_s_setprio(2);
   auto tick = [&](int k) {
     if (COUNT) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1001,6 +1006,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       ts.sp = 0;
     }
     phase(1);
+    __builtin_amdgcn_s_setprio(0);  // trace_run raised it
     if (ts.node >= 0 || ts.sp > 0) continue;  // traversal suspended: resume next iteration
     ts.on = false;
     if (COUNT) simd_tick(cnt, 12, 13);
