@@ -3,7 +3,7 @@ set -e
 cd "$(dirname "$0")/../raytracer-weekend_amd"
 mkdir -p /tmp/isa
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -fno-gpu-rdc -fno-slp-vectorize \
-  -mllvm -amdgpu-atomic-optimizer-strategy=None --cuda-device-only -S csrc/rtw_kernel.hip -o /tmp/isa/k.s "$@" 2>/dev/null
+  -mllvm -amdgpu-atomic-optimizer-strategy=None -mllvm -amdgpu-sched-strategy=max-ilp --cuda-device-only -S csrc/rtw_kernel.hip -o /tmp/isa/k.s "$@" 2>/dev/null
 python3 - <<'PY'
 import re
 txt = open('/tmp/isa/k.s').read()
