@@ -7,10 +7,12 @@
 
 A step = one full frame of the configured workload (default: BASELINE.json configs[1],
 RTOW final random-spheres "jumpy-balls", 1920x1080, 512 spp, 50 bounces) rendered by the
-hot path, with the scene already resident in HBM.  The frame's 8x8 tiles are dealt
-round-robin to the N ranks (one process per GPU, rtw_tile_partition); each rank renders its
-tiles with rtw_render_device, then one RCCL all-gather over xGMI brings every rank's packed
-tiles to all ranks and rank 0 unpacks the framebuffer and copies it to the host.  Total work
+hot path, with the scene already resident in HBM.  On one GPU the frame renders straight into
+the device image (rtw_render_device without tile ids, rtw_render's path).  On N GPUs the frame's
+8x8 tiles are dealt round-robin to the N ranks (one process per GPU, rtw_tile_partition); each
+rank renders its tiles with rtw_render_device, then one RCCL all-gather over xGMI brings every
+rank's packed tiles to all ranks and rank 0 unpacks the framebuffer.  Rank 0 copies the frame
+to the host inside the timed step.  Total work
 is fixed as N grows ("scaling": "strong").  value = rays of the frame (world.hit queries,
 lib.rs:102, counted exactly by the kernel) / max-over-ranks step time.
 
@@ -234,6 +236,9 @@ def main() -> int:
         if multi:
             rt.render_multi(multi)  # blocking: renders, gathers over RCCL, copies the frame to the host
             return
+        if world == 1 and launches == 1:  # one GPU: the whole frame straight into the image (rtw_render's path)
+            rt.render_device(image.data_ptr(), dev, 0, 0, stream.cuda_stream)
+            return
         for k in range(launches):
             a, b = int(bounds[k]), int(bounds[k + 1])
             rt.render_device(packed[a:].data_ptr(), dev, ids[a:].data_ptr(), b - a, stream.cuda_stream)
@@ -253,7 +258,7 @@ def main() -> int:
             if rank == 0:
                 rtw.unpack_tiles_device(w, h, all_ids.data_ptr(), world * per_rank, gathered.data_ptr(),
                                         image.data_ptr(), dev, stream.cuda_stream)
-        else:
+        elif launches > 1:
             rtw.unpack_tiles_device(w, h, ids.data_ptr(), n_mine, packed.data_ptr(), image.data_ptr(), dev,
                                     stream.cuda_stream)
         if rank == 0:
