@@ -168,7 +168,17 @@ struct Builder {
         DevPrim p;
         memset(&p, 0, sizeof p);
         p.type_inst = PT_SPHERE;
-        memcpy(p.q0, n.f, 4 * sizeof(float));
+        // q0 = (c, r * r), q1 = (0, 0, 0, key bits), q2 = (0, 1, r): the layout of a moving sphere
+        // with c1 - c0 = 0 over the unit shutter (rtw_device.hpp), so sphere-only kernels test both
+        // kinds alike; r * r is the f32 product spherical.rs:29 forms per call
+        memcpy(p.q0, n.f, 3 * sizeof(float));
+        {
+          const volatile float r = n.f[3];
+          p.q0[3] = r * r;
+        }
+        p.q2[0] = 0.0f;
+        p.q2[1] = 1.0f;
+        p.q2[2] = n.f[3];
         p.mat = n.mat;
         float r = fabsf(n.f[3]);  // |r|: spherical.rs:98-103 inverts the box for r < 0
         Box b;
@@ -188,9 +198,9 @@ struct Builder {
         memcpy(p.q0, n.f, 3 * sizeof(float));
         p.q0[3] = n.f[8] * n.f[8];
         for (int a = 0; a < 3; ++a) p.q1[a] = n.f[4 + a] - n.f[a];
-        p.q1[3] = n.f[8];
         p.q2[0] = n.f[3];
         p.q2[1] = n.f[7];
+        p.q2[2] = n.f[8];  // r; q1[3] gets the key bits once keys are assigned
         uint32_t t0_bits;
         memcpy(&t0_bits, &n.f[3], 4);
         p.aux = (t0_bits == 0u && n.f[7] == 1.0f) ? 1u : 0u;
@@ -597,6 +607,11 @@ int flatten(Scene& s) {
         f.prims[k].aux = (uint32_t)k;
       }
     f.tshade.swap(by_prim);
+  }
+  // spheres carry their DFS key in q1[3] too (the sphere-only kernels' 32-B test, rtw_device.hpp)
+  for (DevPrim& p : f.prims) {
+    const uint32_t t = p.type_inst & 0xffu;
+    if (t == PT_SPHERE || t == PT_MSPHERE) memcpy(&p.q1[3], &p.key, sizeof p.key);
   }
   // shading records (one per prim, same order)
   for (const DevPrim& p : f.prims) {

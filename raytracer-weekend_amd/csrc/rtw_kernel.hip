@@ -396,6 +396,23 @@ template <bool COUNT, uint32_t FEAT, bool LOCAL = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
                                           uint32_t* cnt, uint64_t seg) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
+  // sphere-only worlds: a static sphere is tested as a moving one with c1 - c0 = 0 (c0 + time * 0 is
+  // c0 up to the sign of a zero coordinate, which changes neither the decision nor t: the zero only
+  // reaches hb, whose sign matters only when every term and sqrt(disc) vanish, a root of +-0 that
+  // fails t >= 0.001 either way), so one branch-free test reads q0 = (c0, r^2) and q1 = (c1 - c0,
+  // key bits) -- 32 B, no type dispatch
+  constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
+  if constexpr (SPH_ONLY && !COUNT) {
+    const float4 q0v = P[0], q1v = P[1];
+    const float t = cand_sphere(wr, center_at(q0v, q1v, P, S.msphere_unit, wr.time), q0v.w);
+    const uint32_t key = __float_as_uint(q1v.w);
+    if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
+      b.t = t;
+      b.key = key;
+      b.prim = (int32_t)pi;
+    }
+    return;
+  }
   // every 16-B part the scene's primitive kinds may need is loaded up front, in one round trip:
   // loading the geometry only after the type was known cost two more dependent trips per test
   const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
@@ -416,7 +433,7 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
   float t = -1.0f;
   if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
-    t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3] * q0[3]);
+    t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3]);  // q0.w = r * r (flattener, the same f32 product)
   } else if ((FEAT & F_MSPHERE) && type == PT_MSPHERE) {
     t = cand_sphere(lr, center_at(q0v, q1v, P, S.msphere_unit, lr.time), q0v.w);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
@@ -671,7 +688,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     const float4* PP = reinterpret_cast<const float4*>(S.prims + b.prim);
     const float4 q0 = PP[0], q1 = PP[1];
     V3 c = type == PT_SPHERE ? mk(q0.x, q0.y, q0.z) : center_at(q0, q1, PP, S.msphere_unit, lr.time);
-    float rad = type == PT_SPHERE ? q0.w : q1.w;
+    const float rad = P.q2[2];  // r (q0.w holds r * r)
     outward = divs(sub(h.p, c), rad);
     if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
