@@ -179,6 +179,7 @@ struct RenderArgs {
   uint32_t tiles_x;           // ceil(w / 8)
   uint32_t slot_base;         // first tile slot of this pass
   uint32_t quota16;           // trace_run returns once quota16/16 of the wave's lanes are done
+  uint32_t leaf16;            // postponed leaves are tested once leaf16/16 of the wave's lanes hold one and are stuck
   uint32_t regen_min;         // regenerate once this many lanes are idle (or every lane is)
   uint32_t batch;             // path ids a wave takes from the global queue per atomic
   uint64_t spp_magic;         // UINT64_MAX / spp + 1 (dev::fastdiv; spp >= 2)
