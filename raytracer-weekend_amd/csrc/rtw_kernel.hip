@@ -32,6 +32,10 @@
 namespace rtw {
 namespace dev {
 
+#ifndef RTW_LDS_SWZ
+#define RTW_LDS_SWZ 0  // LDS node table: XOR-swizzle each node's 16-B slots by node bits 1..3
+#endif
+
 #ifndef RTW_DIEL_PRE
 #define RTW_DIEL_PRE 1  // Dielectric 1 / ir and r0 precomputed by the flattener (DevShade::a)
 #endif
@@ -510,10 +514,13 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // internal nodes (nearest hit child next, the other hit children pushed); a lane that reaches a
 // leaf parks it (one slot; further leaves go on the stack) and keeps walking speculatively until
 // every lane of the wave holds a leaf or has run dry; phase 2 tests all parked leaves together.
-template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT>
+// NCAP > 0: the whole node table is in the workgroup's LDS (`lnodes`, copied at kernel start), so
+// the 7 node loads of a visit are ds_read_b128s instead of vector-memory loads (TA/TD were 89/98%
+// busy on jumpy-balls with the nodes in L1/L2).
+template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
-                          unsigned long long* err, uint64_t* tph) {
+                          unsigned long long* err, uint64_t* tph, const float4* lnodes) {
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   // Waves walking the tree issue before waves shading or regenerating (the path kernel drops the
@@ -538,7 +545,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   // from the uniform table base: the loads take the SGPR-base + VGPR-offset form)
   const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
-  const char* const NB = reinterpret_cast<const char*>(S.nodes);
+  const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes) : reinterpret_cast<const char*>(S.nodes);
   // every wave must drain: a corrupt tree (a cycle) ends the walk instead of hanging the GPU, and
   // raises the launch's error flag (counters[30]), which the host turns into RTW_EINVAL
   constexpr uint32_t GUARD = 1u << 20;
@@ -551,7 +558,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         int32_t top = 0;
         if (can) {
           const int32_t i = ts.sp - 1;
-          top = stk[(SPILL ? min(i, STACK) : i) * BLOCK];
+          top = stk[(SPILL ? min(i, STACK) : i) * BLK];
           if (SPILL && i >= STACK) top = spill[(size_t)(i - STACK) * spill_lanes];  // rare
         }
         const bool popn = can && top >= 0;
@@ -577,13 +584,17 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       if ((uint32_t)__popcll(__ballot(ts.node < 0 && ts.pend != 0)) >= leaf_thr) break;
       if (ts.node >= 0) {
         const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
-        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
-        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
-        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
-        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
-        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
-        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
-        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + 96u));
+        // LDS table, swizzled: a node's 16-B slot f sits at f ^ (node bits 1..3), so lanes reading the
+        // same field of different nodes spread over the 16 bank slots of a 256-B LDS row (unswizzled,
+        // every even node's field f shares one slot: up to 8-way ds_read_b128 conflicts)
+        const uint32_t sw = (NCAP > 0 && RTW_LDS_SWZ) ? (((uint32_t)ts.node << 3) & 0x70u) : 0u;
+        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb | (nx ^ sw)));
+        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb | (fx ^ sw)));
+        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb | (ny ^ sw)));
+        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb | (fy ^ sw)));
+        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb | (nz ^ sw)));
+        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb | (fz ^ sw)));
+        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb | (96u ^ sw)));
         if (COUNT) {
           cnt[0]++;
           simd_tick(cnt, 8, 9);
@@ -632,7 +643,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           // branch-free: a child that is not pushed is written where the next push (or nothing)
           // lands, i.e. at or above the final top, never below it.  Rows 0..STACK exist; with
           // SPILL, row STACK is scratch and entries from STACK up live in HBM (sp < stack_need).
-          stk[(SPILL ? min(sp, STACK) : sp) * BLOCK] = CW[k];
+          stk[(SPILL ? min(sp, STACK) : sp) * BLK] = CW[k];
           if (SPILL && pk && sp >= STACK) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // rare
           sp += pk ? 1 : 0;
         }
@@ -933,11 +944,20 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   return true;
 }
 
-template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT>
-__global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
-  __shared__ int32_t stk_all[(STACK + 1) * BLOCK];  // + 1: trace_run's branch-free push
+// BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
+// waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
+template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0>
+__global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
+  __shared__ int32_t stk_all[(STACK + 1) * BLK];  // + 1: trace_run's branch-free push
+  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * 8 : 1];
+  if constexpr (NCAP > 0) {  // the host launches this variant only for n_nodes <= NCAP
+    const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
+    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
+      nodes_lds[RTW_LDS_SWZ ? (k ^ ((k >> 4) & 7u)) : k] = g[k];  // see trace_run
+    __syncthreads();
+  }
   int32_t* stk = stk_all + threadIdx.x;
-  int32_t* spill = a.spill + (size_t)blockIdx.x * BLOCK + threadIdx.x;  // unused unless spill_depth > 0
+  int32_t* spill = a.spill + (size_t)blockIdx.x * BLK + threadIdx.x;  // unused unless spill_depth > 0
   const uint32_t lane = threadIdx.x & 63u;
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
@@ -946,7 +966,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
   // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
-  __shared__ uint64_t pool_lds[BLOCK / 64][3];
+  __shared__ uint64_t pool_lds[BLK / 64][3];
   uint64_t* const pool = pool_lds[threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
   bool exhausted = false;                // wave-uniform
@@ -1022,8 +1042,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, leaf_thr, st.rng,
-                                           a.counters + 30, ph + 4);
+      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, leaf_thr,
+                                                      st.rng, a.counters + 30, ph + 4, nodes_lds);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1306,8 +1326,13 @@ static int env_int(const char* k, int dflt) {
 }
 struct Variant {
   path_fn fn;
-  uint32_t stack;  // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
+  uint32_t stack;        // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
+  uint32_t block = 256;  // workgroup size fn is compiled for
 };
+// LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
+// waves/SIMD = 3 per CU: (16 + 1) stack rows x 512 x 4 B + 144 node4s x 128 B + the pool words =
+// 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB).
+constexpr int LDSN_STACK = 16, LDSN_CAP = 144, LDSN_BLK = 512;
 template <bool C, uint32_t F>
 static Variant pick5(uint32_t need) {
   using namespace dev;
@@ -1319,7 +1344,7 @@ static Variant pick5(uint32_t need) {
   return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
 }
 template <bool C>
-static Variant pick_kernel(uint32_t feat, uint32_t need, bool list) {
+static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -1343,6 +1368,9 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list) {
       return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
     case 6:
+      if (sph && need <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP && env_int("RTW_LDS_NODES", 1))
+        return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
+                (uint32_t)LDSN_BLK};
       if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
       [[fallthrough]];
     default:
@@ -1354,15 +1382,17 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list) {
       return pick5<C, F_ALL>(need);
   }
 }
-static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need, bool list) {
-  return count ? pick_kernel<true>(feat, need, list) : pick_kernel<false>(feat, need, list);
+static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need, bool list, uint32_t n_nodes) {
+  return count ? pick_kernel<true>(feat, need, list, n_nodes) : pick_kernel<false>(feat, need, list, n_nodes);
 }
 
-static int resident_grid(DeviceCopy& c, path_fn fn, bool count) {
+static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
   int& g = c.grid[count ? 1 : 0];
-  if (g > 0) return g;
+  void*& gf = c.grid_fn[count ? 1 : 0];
+  if (g > 0 && gf == (void*)fn) return g;
+  gf = (void*)fn;
   int per_cu = 0, cus = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, dev::BLOCK, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)block, 0);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
   g = per_cu * cus;
@@ -1435,7 +1465,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need, sc.flat.nodes4.empty());
+    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need, sc.flat.nodes4.empty(),
+                                            (uint32_t)sc.flat.nodes4.size());
     const path_fn fn = var.fn;
     // Regenerate paths only once >= regen_min lanes of a wave are idle (or all are): start_path
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
@@ -1444,10 +1475,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     // iteration) lose with deep deferral: 8 (cornell list variant at 8 waves/SIMD: 29.3k at 1, 29.4k at 4, 29.8k at 8, 28.1k at 24).
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
     a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
-    const int grid = resident_grid(c, fn, count);
+    const int grid = resident_grid(c, fn, var.block, count);
     const uint32_t lds = var.stack;
     a.spill_depth = sc.flat.stack_need > lds ? sc.flat.stack_need - lds : 0;
-    a.spill_lanes = (uint32_t)grid * dev::BLOCK;
+    a.spill_lanes = (uint32_t)grid * var.block;
     const size_t spill_bytes = (size_t)a.spill_depth * a.spill_lanes * sizeof(int32_t);
     if (spill_bytes > c.spill_bytes) {  // first render of a deep tree only
       if (c.spill) HIPCHK(hipFree(c.spill), "hipFree(stack spill)");
@@ -1466,7 +1497,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
       HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
-      hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::BLOCK), 0, stream, a);
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
       HIPCHK(hipGetLastError(), "path_kernel launch");
       HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
       c.kev_head = (c.kev_head + 1) % 64u;

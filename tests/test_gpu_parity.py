@@ -114,12 +114,13 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
 
 @pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16",
                                   "RTW_LIST_MAX=0", "RTW_LIST_MAX=64", "RTW_LIST_OCC=6", "RTW_LEAF16=1",
-                                  "RTW_LEAF16=16"])
+                                  "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
     operations are keyed by its (pixel, sample) id, so the image and the ray count must not move.
-    Same for list mode vs BVH (RTW_LIST_MAX): closest hit with ties to the later object is a
+    Same for the node table in LDS vs global memory (RTW_LDS_NODES) and the occupancy variants
+    (RTW_OCC).  Same for list mode vs BVH (RTW_LIST_MAX): closest hit with ties to the later object is a
     commutative reduction over the leaves, whatever culls them."""
     k, v = knob.split("=")
     monkeypatch.setenv(k, v)
