@@ -19,6 +19,7 @@
 // next sample in the same iteration, so lanes stay busy across paths of 1..50 bounces.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1396,6 +1397,8 @@ static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) 
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
   g = per_cu * cus;
+  if (env_int("RTW_VERBOSE", 0))
+    fprintf(stderr, "rtw: path kernel %p: block %u, %d resident blocks per CU x %d CUs\n", (void*)fn, block, per_cu, cus);
   return g;
 }
 
