@@ -285,7 +285,8 @@ int rtw_scene_dump(const rtw_scene* s, char* buf, size_t cap, size_t* needed);
 int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32_t* w, uint32_t* h);
 /* 0 leaf primitives, 1 materials, 2 textures, 3 BVH nodes, 4 BVH depth, 5 always-tested
  * primitives, 6 instances, 7 BVH2 nodes, 8 traversal-stack bound, 9 feature mask (rtw_device.hpp
- * Feature; selects the path-kernel variant), 10 Perlin tables.  7-9 are valid once rtw_scene_commit has flattened
+ * Feature; selects the path-kernel variant), 10 Perlin tables, 11 stack bound of the sorted-push
+ * walk (LDS-node kernels).  7-9 and 11 are valid once rtw_scene_commit has flattened
  * the scene (also when its upload failed for lack of a device). */
 int64_t rtw_scene_info(const rtw_scene* s, int what);
 

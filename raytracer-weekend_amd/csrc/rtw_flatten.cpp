@@ -439,7 +439,10 @@ struct Collapse {
     return c;
   }
   // returns the node4 index; *bound = worst-case stack entries pushed below (and at) this node
-  int32_t build(int32_t root2, uint32_t* bound) {
+  // *bound4: the same for the sorted-push walk of the LDS-node kernels (trace_run, K16), which writes
+  // a 4-entry window at the stack top on every visit and walks into the nearest hit child: rows
+  // needed = max over root-to-node paths of sum(children - 1) over the ancestors + 4
+  int32_t build(int32_t root2, uint32_t* bound, uint32_t* bound4) {
     std::vector<C> ch;
     const DevNode& r = n2[root2];
     ch.push_back(child(r, 0));
@@ -463,16 +466,17 @@ struct Collapse {
       nd.hi_x[k] = nd.hi_y[k] = nd.hi_z[k] = -INFINITY;
     }
     out.push_back(nd);
-    uint32_t below = 0;
+    uint32_t below = 0, below4 = 0;
     bool inner = false;
     for (size_t k = 0; k < ch.size(); ++k) {
       int32_t word;
       if (ch[k].count) {
         word = (int32_t)~(((uint32_t)ch[k].idx << 3) | ch[k].count);
       } else {
-        uint32_t b = 0;
-        word = build(ch[k].idx, &b);
+        uint32_t b = 0, b4 = 0;
+        word = build(ch[k].idx, &b, &b4);
         below = std::max(below, b);
+        below4 = std::max(below4, b4);
         inner = true;
       }
       DevNode4& o = out[id];
@@ -484,6 +488,7 @@ struct Collapse {
     // a visit pushes every hit child except the nearest internal one, which it walks into next
     // (trace_run); with no internal child it may push them all
     *bound = inner ? (uint32_t)ch.size() - 1 + below : (uint32_t)ch.size();
+    *bound4 = std::max(4u, inner ? (uint32_t)ch.size() - 1 + below4 : 4u);
     return id;
   }
 };
@@ -656,8 +661,9 @@ int flatten(Scene& s) {
   if (!f.nodes.empty()) {
     if (rest.size() >= (1u << 28)) return fail(RTW_EINVAL, "too many BVH primitives for leaf words");
     Collapse col{f.nodes, f.nodes4};
-    uint32_t bound = 0;
-    col.build(0, &bound);
+    uint32_t bound = 0, bound4 = 0;
+    col.build(0, &bound, &bound4);
+    f.stack_need4 = bound4;
     if (f.nodes4.size() >= (1u << 25)) return fail(RTW_EINVAL, "BVH4 too large for 32-bit node offsets");
     f.stack_need = bound;  // entries beyond the kernel's LDS stack spill to a per-lane HBM area
     if (f.stack_need > 4096) return fail(RTW_EINVAL, "BVH4 stack bound %u is unreasonable", f.stack_need);

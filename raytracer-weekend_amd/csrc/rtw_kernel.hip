@@ -33,10 +33,6 @@
 namespace rtw {
 namespace dev {
 
-#ifndef RTW_LDS_SWZ
-#define RTW_LDS_SWZ 0  // LDS node table: XOR-swizzle each node's 16-B slots by node bits 1..3
-#endif
-
 #ifndef RTW_DIEL_PRE
 #define RTW_DIEL_PRE 1  // Dielectric 1 / ir and r0 precomputed by the flattener (DevShade::a)
 #endif
@@ -518,10 +514,23 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // NCAP > 0: the whole node table is in the workgroup's LDS (`lnodes`, copied at kernel start), so
 // the 7 node loads of a visit are ds_read_b128s instead of vector-memory loads (TA/TD were 89/98%
 // busy on jumpy-balls with the nodes in L1/L2).
+//
+// NCAP > 0 also switches to the sorted-push walk over 16-bit stack entries (`stk16`, rows of BLK
+// halfwords).  The LDS copy of the node table replaces each child word by a 14-bit code (internal:
+// the node4 index; leaf: 0x2000 | first << 3 | count), and a visit
+//   * keys every hit child as (its entry distance's float bits, top 16) | code, a miss as 0,
+//   * sorts the 4 keys descending (10 min/max) and writes all four codes to stack rows sp..sp+3
+//     (one address, constant offsets; rows past the new top are scratch: Flat::stack_need4),
+//   * walks into the nearest hit child (the smallest non-zero key) and keeps the others pushed,
+//     farthest deepest; a nearest leaf is parked, or stays pushed if the parking slot is taken.
+// It replaces the per-child nearest / push bookkeeping of the 32-bit walk (~50 VALU per visit).
+// Which nodes are visited in which order never changes the answer (closest hit, ties to the
+// larger key, over every leaf not culled).
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
-                          unsigned long long* err, uint64_t* tph, const float4* lnodes) {
+                          unsigned long long* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
+  constexpr bool K16 = NCAP > 0;
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   // Waves walking the tree issue before waves shading or regenerating (the path kernel drops the
@@ -554,7 +563,16 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   for (; guard < GUARD; ++guard) {
     uint32_t g2 = 0;
     for (; g2 < GUARD; ++g2) {
-      {  // refill from the stack: an internal node, or a parked leaf if the slot is free
+      if constexpr (K16) {  // refill: pop a code (internal node, or a leaf if the parking slot is free)
+        const bool can = ts.node < 0 && ts.sp > 0;
+        const int32_t top = can ? (int32_t)stk16[(ts.sp - 1) * BLK] : 0;
+        const bool leaf = (top & 0x2000) != 0;
+        const bool popn = can && !leaf;
+        const bool popl = can && leaf && ts.pend == 0;
+        ts.node = popn ? top : ts.node;
+        ts.pend = popl ? top : ts.pend;
+        ts.sp -= (popn || popl) ? 1 : 0;
+      } else {  // refill from the stack: an internal node, or a parked leaf if the slot is free
         const bool can = ts.node < 0 && ts.sp > 0;
         int32_t top = 0;
         if (can) {
@@ -585,17 +603,13 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       if ((uint32_t)__popcll(__ballot(ts.node < 0 && ts.pend != 0)) >= leaf_thr) break;
       if (ts.node >= 0) {
         const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
-        // LDS table, swizzled: a node's 16-B slot f sits at f ^ (node bits 1..3), so lanes reading the
-        // same field of different nodes spread over the 16 bank slots of a 256-B LDS row (unswizzled,
-        // every even node's field f shares one slot: up to 8-way ds_read_b128 conflicts)
-        const uint32_t sw = (NCAP > 0 && RTW_LDS_SWZ) ? (((uint32_t)ts.node << 3) & 0x70u) : 0u;
-        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb | (nx ^ sw)));
-        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb | (fx ^ sw)));
-        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb | (ny ^ sw)));
-        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb | (fy ^ sw)));
-        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb | (nz ^ sw)));
-        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb | (fz ^ sw)));
-        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb | (96u ^ sw)));
+        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
+        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
+        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
+        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
+        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
+        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
+        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + 96u));
         if (COUNT) {
           cnt[0]++;
           simd_tick(cnt, 8, 9);
@@ -616,6 +630,34 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           const float f = __builtin_fmaf(FZ[k], inv.z, -ood.z);
           tn[k] = fmaxf(fmaxf(fmaxf(a, b), c), 0.0f);
           hit[k] = tn[k] <= fminf(fminf(fminf(d, e), f), tmax_c);
+        }
+        if constexpr (K16) {
+          // pin the child codes in registers: otherwise the compiler sinks each child's LDS read under
+          // its `hit` branch (4 dependent read round trips per visit)
+          int32_t cwv[4] = {CW[0], CW[1], CW[2], CW[3]};
+          asm volatile("" : "+v"(cwv[0]), "+v"(cwv[1]), "+v"(cwv[2]), "+v"(cwv[3]));
+          uint32_t key[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) key[k] = hit[k] ? ((__float_as_uint(tn[k]) & 0xFFFF0000u) | (uint32_t)cwv[k]) : 0u;
+          const uint32_t a0 = max(key[0], key[1]), b0 = min(key[0], key[1]);
+          const uint32_t c0 = max(key[2], key[3]), d0 = min(key[2], key[3]);
+          const uint32_t s0 = max(a0, c0), x0 = min(a0, c0), y0 = max(b0, d0), s3 = min(b0, d0);
+          const uint32_t s1 = max(x0, y0), s2 = min(x0, y0);
+          uint16_t* w = stk16 + ts.sp * BLK;  // rows sp .. sp + 3 (ds_write_b16 stores the code bits)
+          w[0] = (uint16_t)s0;
+          w[BLK] = (uint16_t)s1;
+          w[2 * BLK] = (uint16_t)s2;
+          w[3 * BLK] = (uint16_t)s3;
+          const bool m1 = s1 != 0u, m2 = s2 != 0u, m3 = s3 != 0u;
+          const uint32_t near = m3 ? s3 : (m2 ? s2 : (m1 ? s1 : s0));
+          const int32_t code = (int32_t)(near & 0x3FFFu);
+          const bool any = s0 != 0u, leaf = (code & 0x2000) != 0;
+          const bool park = any && leaf && ts.pend == 0;
+          // pushed: the hits but the nearest (h - 1), + the nearest leaf if it cannot be parked
+          ts.sp += (int32_t)m1 + (int32_t)m2 + (int32_t)m3 + ((any && leaf && !park) ? 1 : 0);
+          ts.pend = park ? code : ts.pend;
+          ts.node = (any && !leaf) ? code : -1;
+          continue;
         }
         // nearest hit internal child -> next node; the other hit children -> stack / parked slot
         int32_t next = -1;
@@ -655,7 +697,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     if (g2 == GUARD) break;
     tick(0);
     if (ts.pend != 0) {  // phase 2
-      const uint32_t v = ~(uint32_t)ts.pend;
+      const uint32_t v = K16 ? ((uint32_t)ts.pend & 0x1FFFu) : ~(uint32_t)ts.pend;
       const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k) test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg);
       ts.pend = 0;
@@ -949,14 +991,25 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
 template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0>
 __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
-  __shared__ int32_t stk_all[(STACK + 1) * BLK];  // + 1: trace_run's branch-free push
+  // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included)
+  __shared__ int32_t stk_all[NCAP > 0 ? 1 : (STACK + 1) * BLK];
+  __shared__ uint16_t stk16_all[NCAP > 0 ? STACK * BLK : 1];
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * 8 : 1];
-  if constexpr (NCAP > 0) {  // the host launches this variant only for n_nodes <= NCAP
+  if constexpr (NCAP > 0) {  // the host launches this variant only for n_nodes <= NCAP, n_prims < 1024
     const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
-    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
-      nodes_lds[RTW_LDS_SWZ ? (k ^ ((k >> 4) & 7u)) : k] = g[k];  // see trace_run
+    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) {
+      float4 q = g[k];
+      if ((k & 7u) == 6u) {  // child words -> 14-bit codes (trace_run)
+        int32_t c[4] = {__float_as_int(q.x), __float_as_int(q.y), __float_as_int(q.z), __float_as_int(q.w)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = c[j] >= 0 ? c[j] : (0x2000 | ~c[j]);
+        q = make_float4(__int_as_float(c[0]), __int_as_float(c[1]), __int_as_float(c[2]), __int_as_float(c[3]));
+      }
+      nodes_lds[k] = q;
+    }
     __syncthreads();
   }
+  uint16_t* stk16 = stk16_all + threadIdx.x;
   int32_t* stk = stk_all + threadIdx.x;
   int32_t* spill = a.spill + (size_t)blockIdx.x * BLK + threadIdx.x;  // unused unless spill_depth > 0
   const uint32_t lane = threadIdx.x & 63u;
@@ -1044,7 +1097,7 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota, leaf_thr,
-                                                      st.rng, a.counters + 30, ph + 4, nodes_lds);
+                                                      st.rng, a.counters + 30, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1331,9 +1384,9 @@ struct Variant {
   uint32_t block = 256;  // workgroup size fn is compiled for
 };
 // LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
-// waves/SIMD = 3 per CU: (16 + 1) stack rows x 512 x 4 B + 144 node4s x 128 B + the pool words =
-// 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB).
-constexpr int LDSN_STACK = 16, LDSN_CAP = 144, LDSN_BLK = 512;
+// waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 144 node4s x 128 B + the pool
+// words = 43,200 B per workgroup, 129,600 B per CU (<= 160 KiB).
+constexpr int LDSN_STACK = 24, LDSN_CAP = 144, LDSN_BLK = 512;
 template <bool C, uint32_t F>
 static Variant pick5(uint32_t need) {
   using namespace dev;
@@ -1345,7 +1398,8 @@ static Variant pick5(uint32_t need) {
   return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
 }
 template <bool C>
-static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes) {
+static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
+                           uint32_t n_prims) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -1369,7 +1423,8 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
     case 6:
-      if (sph && need <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP && env_int("RTW_LDS_NODES", 1))
+      if (sph && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP && n_prims < 1024u &&
+          env_int("RTW_LDS_NODES", 1))
         return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
                 (uint32_t)LDSN_BLK};
       if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
@@ -1383,8 +1438,11 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return pick5<C, F_ALL>(need);
   }
 }
-static Variant path_kernel_variant(bool count, uint32_t feat, uint32_t need, bool list, uint32_t n_nodes) {
-  return count ? pick_kernel<true>(feat, need, list, n_nodes) : pick_kernel<false>(feat, need, list, n_nodes);
+static Variant path_kernel_variant(bool count, const Flat& f, uint32_t n_prims) {
+  const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
+  const bool list = f.nodes4.empty();
+  return count ? pick_kernel<true>(feat, need, list, nn, need4, n_prims)
+               : pick_kernel<false>(feat, need, list, nn, need4, n_prims);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
@@ -1468,8 +1526,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const Variant var = path_kernel_variant(count, sc.flat.features, sc.flat.stack_need, sc.flat.nodes4.empty(),
-                                            (uint32_t)sc.flat.nodes4.size());
+    const Variant var = path_kernel_variant(count, sc.flat, c.scene.n_prims);
     const path_fn fn = var.fn;
     // Regenerate paths only once >= regen_min lanes of a wave are idle (or all are): start_path
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
