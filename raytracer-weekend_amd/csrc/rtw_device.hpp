@@ -52,14 +52,17 @@ struct alignas(16) DevNode {
 };
 static_assert(sizeof(DevNode) == 64, "DevNode must be 64 B");
 
-// 4-wide BVH node used by the kernel (collapsed from the SAH BVH2).  Planes are stored per axis
+// 4-wide BVH node used by the kernel (collapsed from the SAH BVH2), numbered breadth-first.  Planes are stored per axis
 // as [lo x4][hi x4] so a lane loads its ray's near and far planes with one dwordx4 each, picking
 // lo or hi by the sign of its direction: no min/max sort in the slab test.  Empty slots have an
 // inverted box (lo = +inf, hi = -inf), which that formulation always misses.
 struct alignas(16) DevNode4 {
   float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
   int32_t child[4];  // >= 0: node4 index; < 0: leaf word ~(first_prim << 3 | count)
-  uint32_t pad[4];
+  // the same children as 16-bit codes for the sorted-push walk of the LDS-node kernels: internal
+  // node4 index (< 2^15), leaf 0x8000 | first_prim << 2 | (count - 1) (first < 2^13, count <= 4),
+  // 0 = empty slot; valid when Flat::codes16
+  uint32_t code[4];
 };
 static_assert(sizeof(DevNode4) == 128, "DevNode4 must be 128 B");
 

@@ -690,6 +690,44 @@ int flatten(Scene& s) {
     }
     for (uint8_t x : seenp)
       if (!x) return fail(RTW_EINVAL, "BVH4 misses a primitive");
+    // Breadth-first node numbering: the nodes every ray visits (the top levels) come first, so a
+    // kernel that keeps only the first K node4s in LDS caches the K most visited ones.  Renumbering
+    // never changes the answer (closest hit over the leaves not culled).
+    {
+      std::vector<int32_t> order{0}, renum(f.nodes4.size(), -1);
+      renum[0] = 0;
+      for (size_t q = 0; q < order.size(); ++q) {
+        const DevNode4& nd = f.nodes4[order[q]];
+        for (int k = 0; k < 4; ++k) {
+          if (nd.lo_x[k] > nd.hi_x[k] || nd.child[k] < 0) continue;
+          renum[nd.child[k]] = (int32_t)order.size();
+          order.push_back(nd.child[k]);
+        }
+      }
+      std::vector<DevNode4> bfs(order.size());
+      for (size_t q = 0; q < order.size(); ++q) {
+        bfs[q] = f.nodes4[order[q]];
+        for (int k = 0; k < 4; ++k)
+          if (bfs[q].lo_x[k] <= bfs[q].hi_x[k] && bfs[q].child[k] >= 0) bfs[q].child[k] = renum[bfs[q].child[k]];
+      }
+      f.nodes4.swap(bfs);
+    }
+    // 16-bit child codes of the sorted-push walk (DevNode4::code): possible when node4 indices fit
+    // 15 bits and every leaf has <= 4 prims starting below 8192
+    f.codes16 = f.nodes4.size() < 0x8000u;
+    for (DevNode4& nd : f.nodes4)
+      for (int k = 0; k < 4; ++k) {
+        nd.code[k] = 0;
+        if (nd.lo_x[k] > nd.hi_x[k]) continue;  // empty slot: 0, its inverted box never hits
+        const int32_t w = nd.child[k];
+        if (w >= 0) {
+          nd.code[k] = (uint32_t)w;
+        } else {
+          const uint32_t v = ~(uint32_t)w, first = v >> 3, cnt = v & 7u;
+          if (cnt > 4u || first >= 0x2000u) f.codes16 = false;
+          nd.code[k] = 0x8000u | ((first & 0x1FFFu) << 2) | ((cnt - 1u) & 3u);
+        }
+      }
   }
   // feature set (selects the specialised kernel)
   uint32_t F = 0;

@@ -517,8 +517,8 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // busy on jumpy-balls with the nodes in L1/L2).
 //
 // NCAP > 0 also switches to the sorted-push walk over 16-bit stack entries (`stk16`, rows of BLK
-// halfwords).  The LDS copy of the node table replaces each child word by a 14-bit code (internal:
-// the node4 index; leaf: 0x2000 | first << 3 | count), and a visit
+// halfwords) of the nodes' 16-bit child codes (DevNode4::code: internal = node4 index, leaf =
+// 0x8000 | first << 2 | (count - 1)), and a visit
 //   * keys every hit child as (its entry distance's float bits, top 16) | code, a miss as 0,
 //   * sorts the 4 keys descending (10 min/max) and writes all four codes to stack rows sp..sp+3
 //     (one address, constant offsets; rows past the new top are scratch: Flat::stack_need4),
@@ -568,7 +568,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       if constexpr (K16) {  // refill: pop a code (internal node, or a leaf if the parking slot is free)
         const bool can = ts.node < 0 && ts.sp > 0;
         const int32_t top = can ? (int32_t)stk16[(ts.sp - 1) * BLK] : 0;
-        const bool leaf = (top & 0x2000) != 0;
+        const bool leaf = (top & 0x8000) != 0;
         const bool popn = can && !leaf;
         const bool popl = can && leaf && ts.pend == 0;
         ts.node = popn ? top : ts.node;
@@ -605,13 +605,18 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       if ((uint32_t)__popcll(__ballot(ts.node < 0 && ts.pend != 0)) >= leaf_thr) break;
       if (ts.node >= 0) {
         const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
-        const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
-        const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
-        const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
-        const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
-        const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
-        const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
-        const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + 96u));
+        constexpr uint32_t CWO = K16 ? 112u : 96u;    // child codes (K16) or child words
+        float4 qnx, qfx, qny, qfy, qnz, qfz;
+        int4 cw;
+        {
+          qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
+          qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
+          qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
+          qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
+          qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
+          qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
+          cw = *reinterpret_cast<const int4*>(NB + (nb + CWO));
+        }
         if (COUNT) {
           cnt[0]++;
           simd_tick(cnt, 8, 9);
@@ -652,8 +657,8 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           w[3 * BLK] = (uint16_t)s3;
           const bool m1 = s1 != 0u, m2 = s2 != 0u, m3 = s3 != 0u;
           const uint32_t near = m3 ? s3 : (m2 ? s2 : (m1 ? s1 : s0));
-          const int32_t code = (int32_t)(near & 0x3FFFu);
-          const bool any = s0 != 0u, leaf = (code & 0x2000) != 0;
+          const int32_t code = (int32_t)(near & 0xFFFFu);
+          const bool any = s0 != 0u, leaf = (code & 0x8000) != 0;
           const bool park = any && leaf && ts.pend == 0;
           // pushed: the hits but the nearest (h - 1), + the nearest leaf if it cannot be parked
           ts.sp += (int32_t)m1 + (int32_t)m2 + (int32_t)m3 + ((any && leaf && !park) ? 1 : 0);
@@ -699,8 +704,9 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     if (g2 == GUARD) break;
     tick(0);
     if (ts.pend != 0) {  // phase 2
-      const uint32_t v = K16 ? ((uint32_t)ts.pend & 0x1FFFu) : ~(uint32_t)ts.pend;
-      const int32_t first = (int32_t)(v >> 3), n = (int32_t)(v & 7u);
+      const uint32_t v = K16 ? (uint32_t)ts.pend : ~(uint32_t)ts.pend;
+      const int32_t first = K16 ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
+      const int32_t n = K16 ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k)
         test_prim<COUNT, FEAT, false, PCAP>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, lprims);
       ts.pend = 0;
@@ -1004,18 +1010,9 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
     const float4* gp = reinterpret_cast<const float4*>(a.scene.prims);
     for (uint32_t k = threadIdx.x; k < a.scene.n_prims * 2u; k += BLK) prims_lds[k] = gp[(k >> 1) * 4u + (k & 1u)];
   }
-  if constexpr (NCAP > 0) {  // the host launches this variant only for n_nodes <= NCAP, n_prims < 1024
+  if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
     const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
-    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) {
-      float4 q = g[k];
-      if ((k & 7u) == 6u) {  // child words -> 14-bit codes (trace_run)
-        int32_t c[4] = {__float_as_int(q.x), __float_as_int(q.y), __float_as_int(q.z), __float_as_int(q.w)};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = c[j] >= 0 ? c[j] : (0x2000 | ~c[j]);
-        q = make_float4(__int_as_float(c[0]), __int_as_float(c[1]), __int_as_float(c[2]), __int_as_float(c[3]));
-      }
-      nodes_lds[k] = q;
-    }
+    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) nodes_lds[k] = g[k];
     __syncthreads();
   }
   uint16_t* stk16 = stk16_all + threadIdx.x;
@@ -1392,6 +1389,7 @@ struct Variant {
   path_fn fn;
   uint32_t stack;        // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
   uint32_t block = 256;  // workgroup size fn is compiled for
+  bool k16 = false;      // LDS-node kernel (sorted-push walk)
 };
 // LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
 // waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 144 node4s x 128 B + the pool
@@ -1412,7 +1410,7 @@ static Variant pick5(uint32_t need) {
 }
 template <bool C>
 static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
-                           uint32_t n_prims) {
+                           uint32_t n_prims, bool codes16) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -1436,14 +1434,14 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
     case 6:
-      if (sph && need4 <= (uint32_t)LDSP_STACK && n_nodes <= (uint32_t)LDSN_CAP && n_prims <= (uint32_t)LDSP_CAP &&
-          env_int("RTW_LDS_NODES", 1) && env_int("RTW_LDS_PRIMS", 1))
+      if (sph && codes16 && need4 <= (uint32_t)LDSP_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
+          n_prims <= (uint32_t)LDSP_CAP && env_int("RTW_LDS_NODES", 1) && env_int("RTW_LDS_PRIMS", 1))
         return {path_kernel<C, LDSP_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP, LDSP_CAP>, (uint32_t)LDSP_STACK,
-                (uint32_t)LDSN_BLK};
-      if (sph && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP && n_prims < 1024u &&
+                (uint32_t)LDSN_BLK, true};
+      if (sph && codes16 && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
           env_int("RTW_LDS_NODES", 1))
         return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
-                (uint32_t)LDSN_BLK};
+                (uint32_t)LDSN_BLK, true};
       if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
       [[fallthrough]];
     default:
@@ -1451,15 +1449,20 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       if (sph) return pick5<C, F_SPHERES>(need);
       if ((feat & ~F_BOXES) == 0) return pick5<C, F_BOXES>(need);
       if ((feat & ~F_SMOKE) == 0) return pick5<C, F_SMOKE>(need);
-      if ((feat & ~F_MESHES) == 0) return pick5<C, F_MESHES>(need);
+      if ((feat & ~F_MESHES) == 0) {
+        // a partial LDS node cache (the top 128 / 376 / 760 node4s, the rest from global memory, sorted-push
+        // walk) measured slower on cow / monument (profiles/r02/experiments, n7): the full-table kernels
+        // are for trees that fit
+        return pick5<C, F_MESHES>(need);
+      }
       return pick5<C, F_ALL>(need);
   }
 }
 static Variant path_kernel_variant(bool count, const Flat& f, uint32_t n_prims) {
   const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
   const bool list = f.nodes4.empty();
-  return count ? pick_kernel<true>(feat, need, list, nn, need4, n_prims)
-               : pick_kernel<false>(feat, need, list, nn, need4, n_prims);
+  return count ? pick_kernel<true>(feat, need, list, nn, need4, n_prims, f.codes16)
+               : pick_kernel<false>(feat, need, list, nn, need4, n_prims, f.codes16);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
@@ -1547,7 +1550,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     const path_fn fn = var.fn;
     // the sorted-push walk of the LDS-node kernels parks fewer leaves early: 5/16 measured best on
     // jumpy-balls (+0.5% over 3; profiles/r02/experiments, n5)
-    if (var.block == (uint32_t)LDSN_BLK) a.leaf16 = (uint32_t)std::min(16, std::max(1, env_int("RTW_LEAF16", 5)));
+    if (var.k16 && sc.flat.features == (sc.flat.features & F_SPHERES))
+      a.leaf16 = (uint32_t)std::min(16, std::max(1, env_int("RTW_LEAF16", 5)));
     // Regenerate paths only once >= regen_min lanes of a wave are idle (or all are): start_path
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
     // (RTW_REGEN_MIN sweep 1..32): 24 is best for open scenes (jumpy-balls +4.3%, cow +1.6%,
