@@ -162,6 +162,9 @@ def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: in
                             "source": issue.get("source")}
     if issue and issue.get("ta_busy"):  # vector-memory units (busy, but not the one binding limit)
         out["vmem_units"] = {"ta_busy": issue["ta_busy"], "td_busy": issue.get("td_busy"), "source": issue.get("source")}
+    if issue and issue.get("lds_active") is not None:  # LDS array (node / sphere tables of the LDS-node kernels)
+        out["lds"] = {"active": issue["lds_active"], "conflict_share": issue.get("lds_conflict_share"),
+                      "source": issue.get("source")}
     return out
 
 
@@ -338,7 +341,7 @@ def main() -> int:
     if vj.exists() and not args.spp:
         d = json.loads(vj.read_text())
         issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit",
-                                        "ta_busy", "td_busy")}
+                                        "ta_busy", "td_busy", "lds_active", "lds_conflict_share")}
         issue["source"] = str(vj.relative_to(ROOT))
     n_launch = launches * passes
     # per launch of this rank (multi-device: device 0's launches, its 1/N share of the frame)

@@ -30,7 +30,8 @@ for c in ${CONFIGS:-jumpy-1080p cornell-800 cow-1080p monument-4k}; do
   i=0
   for set in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" \
              "SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_BUSY_CYCLES SQ_INSTS_VMEM_WR TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum" \
-             "TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_WAIT_INST_LDS"; do
+             "TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_WAIT_INST_LDS" \
+             "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     timeout -s KILL 180 rocprofv3 --pmc $set --kernel-trace --output-format csv --kernel-include-regex "path_kernel<false" \
       -d $O/sq$i -o sq -- python3 $R/bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline > $O/sq$i.log 2>&1 || { tail -5 $O/sq$i.log; exit 1; }

@@ -58,7 +58,7 @@ def main():
                "source": str(d.relative_to(ROOT))}
         (ROOT / "profiles" / f"pmc_{cfg}.json").write_text(json.dumps(pub, indent=1))
         c = {}
-        for i in (1, 2, 3):
+        for i in (1, 2, 3, 4):
             f = s / f"sq{i}" / "sq_counter_collection.csv"
             if not f.exists():
                 continue
@@ -78,6 +78,10 @@ def main():
                 # TA / TD busy: cycles summed over the 256 CUs vs GRBM_GUI_ACTIVE summed over the 8 XCDs
                 "ta_busy": round(c["TA_TA_BUSY_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "TA_TA_BUSY_sum" in c else None,
                 "td_busy": round(c["TD_TD_BUSY_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "TD_TD_BUSY_sum" in c else None,
+                # LDS array: active cycles summed over the 256 CUs vs GRBM_GUI_ACTIVE, and the share of them
+                # spent on bank conflicts (MI355X_MICROARCH.md §LDS)
+                "lds_active": round(c["SQ_LDS_IDX_ACTIVE"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "SQ_LDS_IDX_ACTIVE" in c else None,
+                "lds_conflict_share": ratio("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"),
                 "counters": {k: round(v) for k, v in sorted(c.items())},
                 "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r02.sh)"}
         (ROOT / "profiles" / f"valu_{cfg}.json").write_text(json.dumps(valu, indent=1))
