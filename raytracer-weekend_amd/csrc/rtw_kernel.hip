@@ -233,10 +233,29 @@ __device__ __forceinline__ float dev_acosf(float x) {  // f32::acos = atan2(sqrt
 struct Ray { V3 o, d; float time; };
 
 // ---- wrapper chains (transformations.rs:23-38, :115-135): world ray -> object ray
+// Wave-uniform loads of scene tables through the constant address space: the backend emits scalar
+// loads (s_load, scalar cache) instead of 64-lane vector loads of one address, which kept the
+// vector-memory units of the list-mode kernel busy (cornell-box: TA 94%, TD 99%).  Reads only: the
+// kernel never writes the scene tables.
+template <class T>
+__device__ __forceinline__ T uload(const T* p) {
+  if constexpr (sizeof(T) == 16) {  // HIP vector types: load the native 4 x 32-bit vector
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 v = *(const __attribute__((address_space(4))) u4*)(p);
+    T t;
+    __builtin_memcpy(&t, &v, 16);
+    return t;
+  } else {
+    return *(const __attribute__((address_space(4))) T*)(p);
+  }
+}
+
+template <bool UNI = false>
 __device__ __forceinline__ Ray to_local(const DevInst* in, Ray r) {
-  const uint32_t n = in->nops;
+  const uint32_t n = UNI ? uload(&in->nops) : in->nops;
   for (uint32_t k = 0; k < n; ++k) {
-    const float4 op = *reinterpret_cast<const float4*>(in->op[k]);
+    const float4* opp = reinterpret_cast<const float4*>(in->op[k]);
+    const float4 op = UNI ? uload(opp) : *opp;
     if (op.x == (float)IO_TRANSLATE) {
       r.o = sub(r.o, mk(op.y, op.z, op.w));
     } else {
@@ -394,7 +413,8 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
 
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
 // PCAP > 0 (sphere-only kernels): q0, q1 of every prim are in the workgroup's LDS (`lp`, 32 B per prim)
-template <bool COUNT, uint32_t FEAT, bool LOCAL = false, int PCAP = 0>
+// UNI: pi is wave-uniform (the always list): scalar loads (uload)
+template <bool COUNT, uint32_t FEAT, bool LOCAL = false, int PCAP = 0, bool UNI = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
                                           uint32_t* cnt, uint64_t seg, const float4* lp = nullptr) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
@@ -405,7 +425,8 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   // key bits) -- 32 B, no type dispatch
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   if constexpr (SPH_ONLY && !COUNT) {
-    const float4 q0v = PCAP > 0 ? lp[2 * pi] : P[0], q1v = PCAP > 0 ? lp[2 * pi + 1] : P[1];
+    const float4 q0v = PCAP > 0 ? lp[2 * pi] : (UNI ? uload(P) : P[0]);
+    const float4 q1v = PCAP > 0 ? lp[2 * pi + 1] : (UNI ? uload(P + 1) : P[1]);
     const float t = cand_sphere(wr, center_at(q0v, q1v, P, S.msphere_unit, wr.time), q0v.w);
     const uint32_t key = __float_as_uint(q1v.w);
     if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
@@ -417,11 +438,11 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   }
   // every 16-B part the scene's primitive kinds may need is loaded up front, in one round trip:
   // loading the geometry only after the type was known cost two more dependent trips per test
-  const uint4 meta = *reinterpret_cast<const uint4*>(P + 3);
-  const float4 q0v = P[0];
+  const uint4 meta = UNI ? uload(reinterpret_cast<const uint4*>(P + 3)) : *reinterpret_cast<const uint4*>(P + 3);
+  const float4 q0v = UNI ? uload(P) : P[0];
   constexpr bool NEED_Q1 = (FEAT & (F_MSPHERE | F_TRI | F_RECT)) != 0, NEED_Q2 = (FEAT & F_TRI) != 0;
-  const float4 q1v = NEED_Q1 ? P[1] : q0v;
-  const float4 q2v = NEED_Q2 ? P[2] : q0v;
+  const float4 q1v = NEED_Q1 ? (UNI ? uload(P + 1) : P[1]) : q0v;
+  const float4 q2v = NEED_Q2 ? (UNI ? uload(P + 2) : P[2]) : q0v;
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
   // object-space ray of the prim's wrapper chain; in BVH leaves recomputed per test (a few
   // flops) rather than cached, which keeps 8 VGPRs free for occupancy
@@ -430,7 +451,7 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     if (inst == S.uni_inst)  // transformations.rs:23-38 with the kernel-uniform offset: no dependent loads
       lr.o = sub(wr.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
     else
-      lr = to_local(S.insts + inst, wr);
+      lr = to_local<UNI>(S.insts + inst, wr);
   }
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
   float t = -1.0f;
@@ -491,16 +512,17 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     uint32_t cur = 0;
     Ray lr = r;
     for (uint32_t k = 0; k < S.n_always; ++k) {
-      const uint32_t pi = S.always[k];
-      const uint32_t inst = S.prims[pi].type_inst >> 8;
+      const uint32_t pi = uload(S.always + k);
+      const uint32_t inst = uload(&S.prims[pi].type_inst) >> 8;
       if (inst != cur) {
-        lr = inst ? to_local(S.insts + inst, r) : r;
+        lr = inst ? to_local<true>(S.insts + inst, r) : r;
         cur = inst;
       }
-      test_prim<COUNT, FEAT, true>(S, pi, lr, ts.b, cnt, seg);
+      test_prim<COUNT, FEAT, true, 0, true>(S, pi, lr, ts.b, cnt, seg);
     }
   } else {
-    for (uint32_t k = 0; k < S.n_always; ++k) test_prim<COUNT, FEAT, false, PCAP>(S, S.always[k], r, ts.b, cnt, seg, lp);
+    for (uint32_t k = 0; k < S.n_always; ++k)
+      test_prim<COUNT, FEAT, false, PCAP, true>(S, uload(S.always + k), r, ts.b, cnt, seg, lp);
   }
   ts.node = S.n_nodes ? 0 : -1;
   ts.pend = 0;
