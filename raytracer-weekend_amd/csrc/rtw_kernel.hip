@@ -625,6 +625,20 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       // waiting until no lane can descend (Aila & Laine's rule).  leaf_thr = 3/16 of the wave's lanes
       // (knob RTW_LEAF16), measured on MI355X against 1..16/16: monument +8%, cow +0.6%, jumpy -0.4%
       if ((uint32_t)__popcll(__ballot(ts.node < 0 && ts.pend != 0)) >= leaf_thr) break;
+#ifdef RTW_UNI_DIAG
+      if (COUNT) {  // diagnostic build: wave-level visits whose visiting lanes share the node (and octant)
+        const uint64_t vis = __ballot(ts.node >= 0);
+        const int src = (int)__ffsll((long long)vis) - 1;
+        const int32_t n0 = __shfl(ts.node, src, 64);
+        const uint32_t oct = nx | ny | nz, o0 = (uint32_t)__shfl((int)oct, src, 64);
+        const bool un = __ballot(ts.node >= 0 && ts.node != n0) == 0;
+        const bool uo = __ballot(ts.node >= 0 && (ts.node != n0 || oct != o0)) == 0;
+        tph[3] += 1;
+        tph[4] += uo ? 1 : 0;
+        tph[5] += un ? 1 : 0;
+        tph[6] += (uint64_t)__popcll(vis);
+      }
+#endif
       if (ts.node >= 0) {
         const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
         constexpr uint32_t CWO = K16 ? 112u : 96u;    // child codes (K16) or child words
@@ -1216,7 +1230,7 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
     if (lane == 0) {
       for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
       atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
-#ifdef RTW_LANE_DIAG
+#if defined(RTW_LANE_DIAG) || defined(RTW_UNI_DIAG)
       for (int k = 7; k < 11; ++k) atomicAdd(a.counters + 13 + k, (unsigned long long)ph[k]);
 #else
       for (int k = 3; k < 7; ++k) atomicAdd(a.counters + 17 + k, (unsigned long long)ph[k]);
