@@ -412,11 +412,10 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
 }
 
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
-// PCAP > 0 (sphere-only kernels): q0, q1 of every prim are in the workgroup's LDS (`lp`, 32 B per prim)
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
-template <bool COUNT, uint32_t FEAT, bool LOCAL = false, int PCAP = 0, bool UNI = false>
+template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
-                                          uint32_t* cnt, uint64_t seg, const float4* lp = nullptr) {
+                                          uint32_t* cnt, uint64_t seg) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   // sphere-only worlds: a static sphere is tested as a moving one with c1 - c0 = 0 (c0 + time * 0 is
   // c0 up to the sign of a zero coordinate, which changes neither the decision nor t: the zero only
@@ -425,8 +424,8 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   // key bits) -- 32 B, no type dispatch
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   if constexpr (SPH_ONLY && !COUNT) {
-    const float4 q0v = PCAP > 0 ? lp[2 * pi] : (UNI ? uload(P) : P[0]);
-    const float4 q1v = PCAP > 0 ? lp[2 * pi + 1] : (UNI ? uload(P + 1) : P[1]);
+    const float4 q0v = UNI ? uload(P) : P[0];
+    const float4 q1v = UNI ? uload(P + 1) : P[1];
     const float t = cand_sphere(wr, center_at(q0v, q1v, P, S.msphere_unit, wr.time), q0v.w);
     const uint32_t key = __float_as_uint(q1v.w);
     if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
@@ -502,9 +501,9 @@ struct TraceState {
   bool on;       // a traversal is in progress
 };
 
-template <bool COUNT, uint32_t FEAT, int PCAP = 0>
+template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
-                                            uint64_t seg, const float4* lp = nullptr) {
+                                            uint64_t seg) {
   ts.b = Best{INFINITY, 0u, -1};
   if (FEAT & F_INST) {
     // the always list is wave-uniform and in DFS order, so a wrapper chain's prims are adjacent
@@ -518,11 +517,11 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
         cur = inst;
       }
-      test_prim<COUNT, FEAT, true, 0, true>(S, pi, lr, ts.b, cnt, seg);
+      test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg);
     }
   } else {
     for (uint32_t k = 0; k < S.n_always; ++k)
-      test_prim<COUNT, FEAT, false, PCAP, true>(S, uload(S.always + k), r, ts.b, cnt, seg, lp);
+      test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg);
   }
   ts.node = S.n_nodes ? 0 : -1;
   ts.pend = 0;
@@ -549,11 +548,10 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // It replaces the per-child nearest / push bookkeeping of the 32-bit walk (~50 VALU per visit).
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
-template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP, int PCAP>
+template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
-                          unsigned long long* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16,
-                          const float4* lprims) {
+                          unsigned long long* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -744,7 +742,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       const int32_t first = K16 ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
       const int32_t n = K16 ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k)
-        test_prim<COUNT, FEAT, false, PCAP>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, lprims);
+        test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg);
       ts.pend = 0;
     }
     tick(1);
@@ -1034,18 +1032,12 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
 
 // BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
-// PCAP: capacity of the LDS prim table (sphere-only kernels: q0, q1 = 32 B per prim; 0 = global).
-template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, int PCAP = 0>
+template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0>
 __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
   // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included)
   __shared__ int32_t stk_all[NCAP > 0 ? 1 : (STACK + 1) * BLK];
   __shared__ uint16_t stk16_all[NCAP > 0 ? STACK * BLK : 1];
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * 8 : 1];
-  __shared__ float4 prims_lds[PCAP > 0 ? PCAP * 2 : 1];
-  if constexpr (PCAP > 0) {  // n_prims <= PCAP (host)
-    const float4* gp = reinterpret_cast<const float4*>(a.scene.prims);
-    for (uint32_t k = threadIdx.x; k < a.scene.n_prims * 2u; k += BLK) prims_lds[k] = gp[(k >> 1) * 4u + (k & 1u)];
-  }
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
     const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) nodes_lds[k] = g[k];
@@ -1133,14 +1125,13 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
     nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
-    if (!ts.on) trace_begin<COUNT, FEAT, PCAP>(S, st.ray, ts, cnt, st.rng, prims_lds);
+    if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     if (!(FEAT & F_LIST)) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP, PCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
-                                                            leaf_thr, st.rng, a.counters + 30, ph + 4, nodes_lds,
-                                                            stk16, prims_lds);
+      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
+                                                      leaf_thr, st.rng, a.counters + 30, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1431,9 +1422,8 @@ struct Variant {
 // waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 144 node4s x 128 B + the pool
 // words = 43,200 B per workgroup, 129,600 B per CU (<= 160 KiB).
 constexpr int LDSN_STACK = 24, LDSN_CAP = 144, LDSN_BLK = 512;
-// + the sphere table (32 B per prim): 18 stack rows x 1 KiB + 144 x 128 B + 512 x 32 B + the pool words =
-// 53,440 B per workgroup, 160,320 B per CU.
-constexpr int LDSP_STACK = 18, LDSP_CAP = 512;
+// (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
+// from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
 template <bool C, uint32_t F>
 static Variant pick5(uint32_t need) {
   using namespace dev;
@@ -1446,7 +1436,7 @@ static Variant pick5(uint32_t need) {
 }
 template <bool C>
 static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
-                           uint32_t n_prims, bool codes16) {
+                           bool codes16) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -1470,10 +1460,6 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
     case 6:
-      if (sph && codes16 && need4 <= (uint32_t)LDSP_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
-          n_prims <= (uint32_t)LDSP_CAP && env_int("RTW_LDS_NODES", 1) && env_int("RTW_LDS_PRIMS", 1))
-        return {path_kernel<C, LDSP_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP, LDSP_CAP>, (uint32_t)LDSP_STACK,
-                (uint32_t)LDSN_BLK, true};
       if (sph && codes16 && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
           env_int("RTW_LDS_NODES", 1))
         return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
@@ -1494,11 +1480,11 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return pick5<C, F_ALL>(need);
   }
 }
-static Variant path_kernel_variant(bool count, const Flat& f, uint32_t n_prims) {
+static Variant path_kernel_variant(bool count, const Flat& f) {
   const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
   const bool list = f.nodes4.empty();
-  return count ? pick_kernel<true>(feat, need, list, nn, need4, n_prims, f.codes16)
-               : pick_kernel<false>(feat, need, list, nn, need4, n_prims, f.codes16);
+  return count ? pick_kernel<true>(feat, need, list, nn, need4, f.codes16)
+               : pick_kernel<false>(feat, need, list, nn, need4, f.codes16);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
@@ -1582,7 +1568,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     }
     a.sbuf = c.sbuf;
     const bool count = flags & RTW_FLAG_COUNT_TRAVERSAL;
-    const Variant var = path_kernel_variant(count, sc.flat, c.scene.n_prims);
+    const Variant var = path_kernel_variant(count, sc.flat);
     const path_fn fn = var.fn;
     // the sorted-push walk of the LDS-node kernels parks fewer leaves early: 5/16 measured best on
     // jumpy-balls (+0.5% over 3; profiles/r02/experiments, n5)

@@ -114,7 +114,7 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
 
 @pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16",
                                   "RTW_LIST_MAX=0", "RTW_LIST_MAX=64", "RTW_LIST_OCC=6", "RTW_LEAF16=1",
-                                  "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_LDS_PRIMS=0", "RTW_OCC=5"])
+                                  "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
