@@ -289,6 +289,10 @@ int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32
  * walk (LDS-node kernels).  7-9 and 11 are valid once rtw_scene_commit has flattened
  * the scene (also when its upload failed for lack of a device). */
 int64_t rtw_scene_info(const rtw_scene* s, int what);
+/* Introspection for the test harness: the flattened 4-wide BVH (DevNode4, 128 B each, breadth-first
+ * numbered; csrc/rtw_device.hpp), valid once rtw_scene_commit has flattened the scene (also when its
+ * upload failed for lack of a device).  *nodes points into the scene (read-only, lives as long as it). */
+int rtw_scene_nodes(const rtw_scene* s, const void** nodes, uint32_t* n_nodes);
 
 #ifdef __cplusplus
 }

@@ -140,6 +140,7 @@ _SIGS = {
                                      _U32]),
     "rtw_scene_dump": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rtw_scene_image": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(_U8), _U32, _U32]),
+    "rtw_scene_nodes": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), _U32]),
     "rtw_scene_info": (C.c_int64, [C.c_void_p, C.c_int]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -398,6 +399,17 @@ class Scene:
 
     def info(self, what: int) -> int:
         return int(lib().rtw_scene_info(self._p, what))
+
+    def nodes(self) -> np.ndarray:
+        """The flattened BVH4 (DevNode4 records, rtw_device.hpp) as a structured array (a copy)."""
+        p, n = C.c_void_p(), C.c_uint32()
+        _check(lib().rtw_scene_nodes(self._p, C.byref(p), C.byref(n)))
+        dt = np.dtype([("lo_x", "<f4", 4), ("hi_x", "<f4", 4), ("lo_y", "<f4", 4), ("hi_y", "<f4", 4),
+                       ("lo_z", "<f4", 4), ("hi_z", "<f4", 4), ("child", "<i4", 4), ("code", "<u4", 4)])
+        if not n.value:
+            return np.zeros(0, dt)
+        buf = (C.c_uint8 * (128 * n.value)).from_address(p.value)
+        return np.frombuffer(bytes(buf), dtype=dt).copy()
 
 
 class Raytracer:

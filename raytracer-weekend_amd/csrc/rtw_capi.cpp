@@ -547,6 +547,12 @@ int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** px, uint32_t
   }
   return fail(RTW_EINVAL, "no image texture #%u", k);
 }
+int rtw_scene_nodes(const rtw_scene* s, const void** nodes, uint32_t* n_nodes) {
+  if (!s || !nodes || !n_nodes) return fail(RTW_EINVAL, "NULL argument");
+  *nodes = s->s.flat.nodes4.empty() ? nullptr : (const void*)s->s.flat.nodes4.data();
+  *n_nodes = (uint32_t)s->s.flat.nodes4.size();
+  return RTW_OK;
+}
 int64_t rtw_scene_info(const rtw_scene* s, int what) {
   if (!s) return -1;
   const Scene& sc = s->s;

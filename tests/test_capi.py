@@ -140,3 +140,47 @@ def test_abi_version_matches_header(rtw):
     import pathlib
     text = (pathlib.Path(__file__).resolve().parents[1] / "include" / "rtw.h").read_text()
     assert int(re.search(r"#define RTW_ABI_VERSION (\d+)", text).group(1)) == rtw.ABI_VERSION
+
+
+def _commit_anywhere(rtw, s):
+    if rtw.device_count() > 0:
+        s.commit()
+    else:
+        with pytest.raises(rtw.RtwError):
+            s.commit()
+
+
+@pytest.mark.parametrize("name", ["jumpy-balls", "wavefront-cow-obj", "textured-monument", "book2-final-scene"])
+def test_bvh4_breadth_first_codes_and_bounds(rtw, name):
+    """rtw_flatten.cpp: node4s are numbered breadth-first (every internal child's index is larger than
+    its parent's and children appear in visit order), each child's 16-bit code (DevNode4::code, the
+    LDS-node kernels' stack entries) decodes to the same child as its 32-bit child word, and the
+    sorted-push walk's stack bound (info 11) covers the 32-bit walk's (info 8) plus its 4-row window
+    over a root-to-leaf path (recomputed here from the nodes)."""
+    s = rtw.Scene()
+    s.preset(name, 16 / 9, seed=3)
+    _commit_anywhere(rtw, s)
+    nd = s.nodes()
+    assert len(nd) == s.info(3) > 0
+    empty = nd["lo_x"] > nd["hi_x"]
+    nxt = 1
+    for i in range(len(nd)):
+        for k in range(4):
+            if empty[i, k]:
+                assert nd["code"][i, k] == 0
+                continue
+            w, c = int(nd["child"][i, k]), int(nd["code"][i, k])
+            if w >= 0:
+                assert w == nxt and c == w  # breadth-first: the next unnumbered index
+                nxt += 1
+            else:
+                v = ~w & 0xFFFFFFFF
+                first, cnt = v >> 3, v & 7
+                assert c & 0x8000 and ((c >> 2) & 0x1FFF) == first and (c & 3) + 1 == cnt
+    assert nxt == len(nd)
+
+    def bound4(i):  # max over paths of sum(children - 1) + 4 (rtw_flatten.cpp Collapse::build)
+        ch = [k for k in range(4) if not empty[i, k]]
+        inner = [int(nd["child"][i, k]) for k in ch if nd["child"][i, k] >= 0]
+        return max(4, len(ch) - 1 + max(bound4(j) for j in inner)) if inner else 4
+    assert s.info(11) == bound4(0) >= s.info(8)
