@@ -253,3 +253,51 @@ def test_console_app_frames(gpu, tmp_path):
         got = np.asarray(Image.open(pngs[k]).convert("RGB"))
         assert got.shape == (height, width, 3)
         assert np.array_equal(got, want), f"camera {k}: {int((got != want).sum())} bytes differ"
+
+
+def _sphere_world(rtw, seed):
+    """A random sphere world in a BvhNode (> list_max leaves, so the BVH kernels run): static and
+    moving spheres (unit and non-unit shutters), negative radii (hollow glass, spherical.rs:98-103),
+    Lambertian / checker / Metal / Dielectric / DiffuseLight materials, a ground sphere."""
+    rng = np.random.default_rng(seed)
+    s = rtw.Scene()
+    mats = [s.lambertian_solid(rng.uniform(0.1, 0.9, 3)) for _ in range(4)]
+    mats += [s.lambertian(s.checker(s.solid_rgb(0.2, 0.3, 0.1), s.solid_rgb(0.9, 0.9, 0.9), 10.0))]
+    mats += [s.metal(rng.uniform(0.5, 1.0, 3), float(f)) for f in (0.0, 0.3)]
+    mats += [s.dielectric(1.5), s.diffuse_light(s.solid_rgb(4.0, 4.0, 4.0))]
+    n = 120
+    c = np.stack([rng.uniform(-6, 6, n), rng.uniform(0.1, 1.2, n), rng.uniform(-6, 6, n)], 1)
+    r = rng.uniform(0.15, 0.4, n)
+    r[rng.random(n) < 0.1] *= -1.0  # hollow glass shells
+    m = rng.integers(0, len(mats), n)
+    mov = rng.random(n) < 0.4
+    with s.bvh(0.0, 1.0):
+        s.sphere((0.0, -1000.0, 0.0), 1000.0, mats[4])
+        s.spheres(c[~mov], r[~mov], m[~mov])
+        k = int(mov.sum())
+        t0 = np.where(rng.random(k) < 0.5, 0.0, 0.25).astype(np.float32)
+        t1 = np.where(rng.random(k) < 0.5, 1.0, 0.75).astype(np.float32)
+        s.moving_spheres(c[mov], t0, c[mov] + rng.uniform(-0.3, 0.3, (k, 3)), t1, r[mov], m[mov])
+    cam = rtw.Camera.new((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, 16 / 9, 0.1, 10.0, 0.0, 1.0)
+    return s, cam, (0.7, 0.8, 1.0)
+
+
+@pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed):
+    """Sphere worlds run the LDS-node kernel (node table in LDS, sorted-push walk over 16-bit codes)
+    when their tree fits, else the global-node one: both bit-exact against the oracle, with equal ray
+    counts, on worlds that mix every sphere kind and material the sphere kernels specialise for."""
+    if knob:
+        k, v = knob.split("=")
+        monkeypatch.setenv(k, v)
+    rtw = gpu
+    s, cam, bg = _sphere_world(rtw, seed)
+    text = s.dump()
+    s.commit()
+    assert s.info(3) > 0 and s.info(11) <= 24  # a BVH, within the LDS-node kernel's 24-row stack
+    w, h, spp = 48, 27, 4
+    g, st = rtw.Raytracer(s, cam, bg, w, h, spp, seed=5).render()
+    ref, rays = orc.OracleScene(text, []).render(orc.camera_from_fields(cam.as_dict()), bg, w, h, spp, seed=5)
+    assert st["rays"] == rays
+    assert np.array_equal(g.view(np.uint32), ref.view(np.uint32))
