@@ -545,7 +545,8 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 //     (one address, constant offsets; rows past the new top are scratch: Flat::stack_need4),
 //   * walks into the nearest hit child (the smallest non-zero key) and keeps the others pushed,
 //     farthest deepest; a nearest leaf is parked, or stays pushed if the parking slot is taken.
-// It replaces the per-child nearest / push bookkeeping of the 32-bit walk (~50 VALU per visit).
+// It replaces the per-child nearest / push bookkeeping of the 32-bit walk (a visit: 97 -> 91 VALU,
+// 44 of them the slab tests) and halves the stack's LDS.
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
