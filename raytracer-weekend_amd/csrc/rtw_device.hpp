@@ -10,7 +10,7 @@
 //                         r=1000 ground sphere) instead of polluting the BVH.
 //   tshade  : DevTriShade per prim (triangles only filled): vertex normals + uvs, read only for the winner.
 //   insts   : DevInst[]   wrapper chains (Translation / YRotation), outer -> inner.
-//   mats, texs, texels   : material / texture tables and RGB8 image data.
+//   mats, texs, texels   : material / texture tables and image data (RGBX8: 4 B per texel).
 #pragma once
 #include <stdint.h>
 

@@ -521,9 +521,14 @@ int flatten(Scene& s) {
     d.type = t.type; d.odd = t.odd; d.even = t.even; d.freq = t.freq;
     memcpy(d.c, t.c, sizeof d.c);
     if (t.type == TT_IMAGE) {
+      // RGBX8 on the device: one aligned 4-byte load per lookup instead of three byte loads
+      if (f.texels.size() + 4ull * t.w * t.h >= (1ull << 32)) return fail(RTW_EINVAL, "image textures exceed 4 GiB");
       d.off = (uint32_t)f.texels.size();
       d.w = t.w; d.h = t.h;
-      f.texels.insert(f.texels.end(), t.img.begin(), t.img.end());
+      const size_t n = (size_t)t.w * t.h;
+      f.texels.resize(f.texels.size() + 4 * n, 0);
+      uint8_t* o = f.texels.data() + d.off;
+      for (size_t q = 0; q < n; ++q) memcpy(o + 4 * q, t.img.data() + 3 * q, 3);
     }
     if (t.type == TT_NOISE) {
       d.off = (uint32_t)f.perlins.size();

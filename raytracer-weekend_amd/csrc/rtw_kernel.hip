@@ -937,9 +937,10 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
       uint32_t j = (fj != fj || fj <= 0.0f) ? 0u : (fj >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fj);
       i = i > t.w - 1 ? t.w - 1 : i;
       j = j > t.h - 1 ? t.h - 1 : j;
-      const uint8_t* px = S.texels + t.off + ((size_t)j * t.w + i) * 3;
+      // image_texture.rs:34-52; texels are RGBX8 on the device (rtw_flatten.cpp): one 4-byte load
+      const uint32_t px = *reinterpret_cast<const uint32_t*>(S.texels + t.off + ((size_t)j * t.w + i) * 4);
       const float sc = 1.0f / 255.0f;
-      return mk((float)px[0] * sc, (float)px[1] * sc, (float)px[2] * sc);
+      return mk((float)(px & 0xffu) * sc, (float)((px >> 8) & 0xffu) * sc, (float)((px >> 16) & 0xffu) * sc);
     }
     if ((FEAT & F_NOISE) && t.type == TT_NOISE) {  // texture.rs:89-95
       const float tb = perlin_turbulence(S.perlins[t.off], p, 7);
