@@ -1421,9 +1421,9 @@ struct Variant {
   bool k16 = false;      // LDS-node kernel (sorted-push walk)
 };
 // LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
-// waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 144 node4s x 128 B + the pool
-// words = 43,200 B per workgroup, 129,600 B per CU (<= 160 KiB).
-constexpr int LDSN_STACK = 24, LDSN_CAP = 144, LDSN_BLK = 512;
+// waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 224 node4s x 128 B + the pool
+// words = 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB): sphere worlds of up to ~850 spheres.
+constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
 // (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
 // from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
 template <bool C, uint32_t F>
