@@ -255,7 +255,7 @@ def test_console_app_frames(gpu, tmp_path):
         assert np.array_equal(got, want), f"camera {k}: {int((got != want).sum())} bytes differ"
 
 
-def _sphere_world(rtw, seed):
+def _sphere_world(rtw, seed, n=120):
     """A random sphere world in a BvhNode (> list_max leaves, so the BVH kernels run): static and
     moving spheres (unit and non-unit shutters), negative radii (hollow glass, spherical.rs:98-103),
     Lambertian / checker / Metal / Dielectric / DiffuseLight materials, a ground sphere."""
@@ -265,7 +265,6 @@ def _sphere_world(rtw, seed):
     mats += [s.lambertian(s.checker(s.solid_rgb(0.2, 0.3, 0.1), s.solid_rgb(0.9, 0.9, 0.9), 10.0))]
     mats += [s.metal(rng.uniform(0.5, 1.0, 3), float(f)) for f in (0.0, 0.3)]
     mats += [s.dielectric(1.5), s.diffuse_light(s.solid_rgb(4.0, 4.0, 4.0))]
-    n = 120
     c = np.stack([rng.uniform(-6, 6, n), rng.uniform(0.1, 1.2, n), rng.uniform(-6, 6, n)], 1)
     r = rng.uniform(0.15, 0.4, n)
     r[rng.random(n) < 0.1] *= -1.0  # hollow glass shells
@@ -283,8 +282,8 @@ def _sphere_world(rtw, seed):
 
 
 @pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0"])
-@pytest.mark.parametrize("seed", [1, 2])
-def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed):
+@pytest.mark.parametrize("seed,n", [(1, 120), (2, 120), (3, 700)])
+def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
     """Sphere worlds run the LDS-node kernel (node table in LDS, sorted-push walk over 16-bit codes)
     when their tree fits, else the global-node one: both bit-exact against the oracle, with equal ray
     counts, on worlds that mix every sphere kind and material the sphere kernels specialise for."""
@@ -292,10 +291,11 @@ def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed):
         k, v = knob.split("=")
         monkeypatch.setenv(k, v)
     rtw = gpu
-    s, cam, bg = _sphere_world(rtw, seed)
+    s, cam, bg = _sphere_world(rtw, seed, n)
     text = s.dump()
     s.commit()
     assert s.info(3) > 0 and s.info(11) <= 24  # a BVH, within the LDS-node kernel's 24-row stack
+    assert (s.info(3) > 144) == (n > 500)  # the 700-sphere world fills more than the old 144-node table
     w, h, spp = 48, 27, 4
     g, st = rtw.Raytracer(s, cam, bg, w, h, spp, seed=5).render()
     ref, rays = orc.OracleScene(text, []).render(orc.camera_from_fields(cam.as_dict()), bg, w, h, spp, seed=5)
