@@ -560,7 +560,8 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   // priority again when trace_run returns).  MI355X A/B (profiles/r02/experiments, s1/s2): jumpy
   // +1.7%, cow +1.6%, monument +0.7%; shading first, node-load issue first or graded levels were
   // slower or equal.
-  __builtin_amdgcn_s_setprio(2);
+  // The LDS-node kernel (NCAP > 0, node loads from LDS) is 0.6% faster without it (experiments, p2).
+  if constexpr (NCAP == 0) __builtin_amdgcn_s_setprio(2);
   auto tick = [&](int k) {
     if (COUNT) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
