@@ -258,7 +258,8 @@ int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* 
 int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
 
 /* Diagnostics: evaluate the render path's f32 transcendentals on the device over n host values
- * (fn 0 log10f(a), 1 sinf(a), 2 acosf(a), 3 atan2f(a, b); DESIGN.md §Parity: correctly rounded).
+ * (fn 0 log10f(a), 1 sinf(a), 2 acosf(a), 3 atan2f(a, b); DESIGN.md §Parity: correctly rounded;
+ * fn 4 a / b by the camera's Markstein division from the reciprocal RN(1 / b)).
  * Used by the parity tests to pin the device functions against the oracle's. */
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
 

@@ -187,6 +187,7 @@ struct RenderArgs {
   uint32_t batch;             // path ids a wave takes from the global queue per atomic
   uint64_t spp_magic;         // UINT64_MAX / spp + 1 (dev::fastdiv; spp >= 2)
   float fw1, fh1;             // (float)(w - 1), (float)(h - 1) (lib.rs:84-85 divisors)
+  float rw1, rh1;             // RN(1 / fw1), RN(1 / fh1): the camera divisions by Markstein's correction
   float time_span;            // cam.time1 - cam.time0 in f32 (UniformFloat scale, camera.rs:72)
   uint64_t tiles_x_magic;     // UINT64_MAX / tiles_x + 1 (tiles_x >= 2)
   const uint32_t* tile_ids;   // device array or nullptr (slot == tile id, full-image output)

@@ -1006,6 +1006,18 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// RN(x / b) from y = RN(1 / b) by Markstein's correction (q0 = RN(x y) is within an ulp of x / b, the
+// residual r = x - q0 b is exact in one fma, and RN(q0 + r y) = RN(x / b); Markstein 1990, no
+// underflow or overflow): the camera's u, v divisions (lib.rs:84-85), whose divisors w - 1, h - 1 are
+// integers in [1, 65535] and dividends 0 or in [2^-24, 65536), with y computed exactly on the host.
+// Three VALU ops instead of the ~10 of an IEEE division; tests/test_gpu_parity.py checks it against
+// IEEE division on the device.
+__device__ __forceinline__ float div_by_recip(float x, float b, float y) {
+  const float q0 = x * y;
+  const float r = __builtin_fmaf(-q0, b, x);
+  return __builtin_fmaf(r, y, q0);
+}
+
 __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
   const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
@@ -1018,8 +1030,8 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   const DevCamera& C = a.cam;
   uint64_t rng = xoro_seed(splitmix64(a.seed_hash ^ (((uint64_t)j << 48) | ((uint64_t)i << 32) | s)));
   // lib.rs:84-86 + camera.rs:66-74
-  const float u = ((float)i + gen_f32(rng)) / a.fw1;
-  const float v = ((float)j + gen_f32(rng)) / a.fh1;
+  const float u = div_by_recip((float)i + gen_f32(rng), a.fw1, a.rw1);
+  const float v = div_by_recip((float)j + gen_f32(rng), a.fh1, a.rh1);
   const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
   const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
   st.ray.o = add(ld3(C.origin), off);
@@ -1274,6 +1286,10 @@ __global__ void libm_kernel(int fn, uint32_t n, const float* a, const float* b, 
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
   const float x = a[g];
+  if (fn == 4) {  // the camera division: Markstein's correction from the IEEE reciprocal (= RN(1 / b))
+    out[g] = div_by_recip(x, b[g], 1.0f / b[g]);
+    return;
+  }
   out[g] = fn == 0 ? dev_log10f(x) : (fn == 1 ? dev_sinf(x) : (fn == 2 ? dev_acosf(x) : dev_atan2f(x, b[g])));
 }
 
@@ -1505,6 +1521,18 @@ static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) 
   return g;
 }
 
+// RN(1 / b) for an integer-valued b in [1, 2^24): the float nearest 1 / b, chosen among the neighbours of
+// the double quotient by the exact residual |1 - y b| (y b is exact in double: 24 x 24 bits)
+static float recip_rn(float b) {
+  float y = (float)(1.0 / (double)b), best = y;
+  double e = fabs(1.0 - (double)y * (double)b);
+  for (float c : {nextafterf(y, 0.0f), nextafterf(y, 2.0f)}) {
+    const double ec = fabs(1.0 - (double)c * (double)b);
+    if (ec < e) { e = ec; best = c; }
+  }
+  return best;
+}
+
 int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
                    uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles, uint32_t n_slots,
                    float* d_out, void* stream_, uint32_t flags, void* ev0_, void* ev1_) {
@@ -1533,6 +1561,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   a.spp_magic = spp > 1u ? UINT64_MAX / spp + 1u : 0u;
   a.fw1 = (float)(w - 1u);
   a.fh1 = (float)(h - 1u);
+  a.rw1 = recip_rn(a.fw1);
+  a.rh1 = recip_rn(a.fh1);
   {
     volatile float t0 = cam->time0, t1 = cam->time1;  // one IEEE f32 subtraction, as on the device
     a.time_span = t1 - t0;
@@ -1805,7 +1835,7 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
 }
 
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out) {
-  if (fn < 0 || fn > 3 || (n && (!a || !out || (fn == 3 && !b)))) return fail(RTW_EINVAL, "bad arguments");
+  if (fn < 0 || fn > 4 || (n && (!a || !out || (fn >= 3 && !b)))) return fail(RTW_EINVAL, "bad arguments");
   if (!n) return RTW_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
@@ -1813,7 +1843,7 @@ int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out
   const size_t bytes = (size_t)n * sizeof(float);
   int rc = RTW_OK;
   if (hipMalloc((void**)&da, bytes) != hipSuccess || hipMalloc((void**)&dout, bytes) != hipSuccess ||
-      (fn == 3 && hipMalloc((void**)&db, bytes) != hipSuccess)) {
+      (fn >= 3 && hipMalloc((void**)&db, bytes) != hipSuccess)) {
     rc = fail(RTW_ENOMEM, "hipMalloc(diag)");
   } else if (hipMemcpy(da, a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
              (db && hipMemcpy(db, b, bytes, hipMemcpyHostToDevice) != hipSuccess)) {

@@ -198,6 +198,28 @@ def test_device_libm_equals_oracle(gpu, orc):
         assert bad.size == 0, (fn, bad.size, a[bad[:4]], dev[bad[:4]], ref[bad[:4]])
 
 
+def test_camera_division_equals_ieee(gpu):
+    """start_path's u = (i + U) / (w - 1), v = (j + U) / (h - 1) (lib.rs:84-85) use Markstein's
+    correction from RN(1 / b) instead of an IEEE division: bit-identical to the IEEE f32 quotient for
+    every dividend the camera forms (0, or i + U with U = k 2^-24) and every divisor 1..65535."""
+    rtw = gpu
+    rng = np.random.default_rng(7)
+    n = 1 << 22
+    i = rng.integers(0, 65536, n).astype(np.float32)
+    U = (rng.integers(0, 1 << 24, n).astype(np.float64) * 2.0 ** -24).astype(np.float32)
+    U[: n // 8] = (np.arange(n // 8) % 64).astype(np.float32) * np.float32(2.0 ** -24)  # tiny draws
+    i[: n // 16] = 0.0
+    a = (i + U).astype(np.float32)  # one IEEE f32 addition, as the kernel forms it
+    b = rng.integers(1, 65536, n).astype(np.float32)
+    b[:1024] = np.arange(1, 1025, dtype=np.float32)
+    b[1024:2048] = np.arange(65535 - 1023, 65536, dtype=np.float32)
+    a[2048:3072] = b[2048:3072]  # exact quotients
+    dev = rtw.diag_libm(4, a, b)
+    ref = (a / b).astype(np.float32)
+    bad = np.nonzero(dev.view(np.uint32) != ref.view(np.uint32))[0]
+    assert bad.size == 0, (bad.size, a[bad[:4]], b[bad[:4]], dev[bad[:4]], ref[bad[:4]])
+
+
 def test_render_stream_pixels(gpu):
     """Raytracer::render() as a Pixel stream (lib.rs:50-76): same sums as rtw_render, emitted
     row j = h-1 .. 0, column 0 .. w-1, band by band; the ProgressMessage frames round-trip."""
