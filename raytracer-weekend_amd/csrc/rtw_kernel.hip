@@ -33,6 +33,10 @@
 namespace rtw {
 namespace dev {
 
+#ifndef RTW_SPH_RCP
+#define RTW_SPH_RCP 1  // sphere roots by Markstein's correction from a per-traversal RN(1 / |d|^2)
+#endif
+
 #ifndef RTW_DIEL_PRE
 #define RTW_DIEL_PRE 1  // Dielectric 1 / ir and r0 precomputed by the flattener (DevShade::a)
 #endif
@@ -267,6 +271,18 @@ __device__ __forceinline__ Ray to_local(const DevInst* in, Ray r) {
   return r;
 }
 
+// RN(x / b) from y = RN(1 / b) by Markstein's correction (q0 = RN(x y) is within an ulp of x / b, the
+// residual r = x - q0 b is exact in one fma, and RN(q0 + r y) = RN(x / b); Markstein 1990, no
+// underflow or overflow): the camera's u, v divisions (lib.rs:84-85), whose divisors w - 1, h - 1 are
+// integers in [1, 65535] and dividends 0 or in [2^-24, 65536), with y computed exactly on the host.
+// Three VALU ops instead of the ~10 of an IEEE division; tests/test_gpu_parity.py checks it against
+// IEEE division on the device.
+__device__ __forceinline__ float div_by_recip(float x, float b, float y) {
+  const float q0 = x * y;
+  const float r = __builtin_fmaf(-q0, b, x);
+  return __builtin_fmaf(r, y, q0);
+}
+
 // ---- candidate t of one primitive (independent of t_max; -1 = miss)
 // rad2 = radius * radius (precomputed for moving spheres; the same f32 product)
 __device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad2) {  // spherical.rs:26-44
@@ -279,6 +295,34 @@ __device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad2) {  
   float sq = sqrtf(disc);
   float root = (-hb - sq) / a;
   if (root < TMIN) root = (-hb + sq) / a;  // root1 > t_max implies root2 > t_max
+  return root;
+}
+// The same test with the ray's a = |d|^2 and y = RN(1 / a) computed once per traversal (SphRcp): each
+// root is Markstein's correction div_by_recip (3 VALU) instead of an IEEE division (~10).  Equal to
+// the IEEE quotient whenever a is in [2^-60, 2^60] and |numerator| < 2^64 (then the quotient is finite,
+// and wherever it is normal the correction is exact; below 2^-126 both are < TMIN); other lanes divide.
+struct SphRcp { float a, ya; bool ok; };
+__device__ __forceinline__ SphRcp sph_rcp(const Ray& r) {
+  SphRcp q;
+  q.a = len2(r.d);
+  q.ya = 1.0f / q.a;
+  q.ok = q.a >= 0x1p-60f && q.a <= 0x1p60f;
+  return q;
+}
+__device__ __forceinline__ float sph_div(float n, const SphRcp& q) {
+  float t = div_by_recip(n, q.a, q.ya);
+  if (__builtin_expect(!(q.ok && fabsf(n) < 0x1p64f), 0)) t = n / q.a;
+  return t;
+}
+__device__ __forceinline__ float cand_sphere_rcp(const Ray& r, V3 c, float rad2, const SphRcp& q) {
+  V3 oc = sub(r.o, c);
+  float hb = dot(oc, r.d);
+  float cc = len2(oc) - rad2;
+  float disc = hb * hb - q.a * cc;
+  if (!(disc >= 0.0f)) return -1.0f;
+  float sq = sqrtf(disc);
+  float root = sph_div(-hb - sq, q);
+  if (root < TMIN) root = sph_div(-hb + sq, q);
   return root;
 }
 // spherical.rs:117-123 over the flattened layout q0 = (c0, r*r), q1 = (c1 - c0, r), q2 = (t0, t1)
@@ -415,7 +459,7 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
 template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
-                                          uint32_t* cnt, uint64_t seg) {
+                                          uint32_t* cnt, uint64_t seg, const SphRcp* rq = nullptr) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   // sphere-only worlds: a static sphere is tested as a moving one with c1 - c0 = 0 (c0 + time * 0 is
   // c0 up to the sign of a zero coordinate, which changes neither the decision nor t: the zero only
@@ -426,7 +470,8 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   if constexpr (SPH_ONLY && !COUNT) {
     const float4 q0v = UNI ? uload(P) : P[0];
     const float4 q1v = UNI ? uload(P + 1) : P[1];
-    const float t = cand_sphere(wr, center_at(q0v, q1v, P, S.msphere_unit, wr.time), q0v.w);
+    const V3 c = center_at(q0v, q1v, P, S.msphere_unit, wr.time);
+    const float t = rq ? cand_sphere_rcp(wr, c, q0v.w, *rq) : cand_sphere(wr, c, q0v.w);
     const uint32_t key = __float_as_uint(q1v.w);
     if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
       b.t = t;
@@ -520,8 +565,12 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
       test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg);
     }
   } else {
+    constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
+    SphRcp rq;
+    if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
     for (uint32_t k = 0; k < S.n_always; ++k)
-      test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg);
+      test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg,
+                                          (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
   }
   ts.node = S.n_nodes ? 0 : -1;
   ts.pend = 0;
@@ -554,6 +603,9 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
                           unsigned long long* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
+  constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
+  SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
+  if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   // Waves walking the tree issue before waves shading or regenerating (the path kernel drops the
@@ -744,7 +796,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       const int32_t first = K16 ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
       const int32_t n = K16 ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k)
-        test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg);
+        test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
       ts.pend = 0;
     }
     tick(1);
@@ -1004,18 +1056,6 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
   return ((uint64_t)hi << 32) | lo;
-}
-
-// RN(x / b) from y = RN(1 / b) by Markstein's correction (q0 = RN(x y) is within an ulp of x / b, the
-// residual r = x - q0 b is exact in one fma, and RN(q0 + r y) = RN(x / b); Markstein 1990, no
-// underflow or overflow): the camera's u, v divisions (lib.rs:84-85), whose divisors w - 1, h - 1 are
-// integers in [1, 65535] and dividends 0 or in [2^-24, 65536), with y computed exactly on the host.
-// Three VALU ops instead of the ~10 of an IEEE division; tests/test_gpu_parity.py checks it against
-// IEEE division on the device.
-__device__ __forceinline__ float div_by_recip(float x, float b, float y) {
-  const float q0 = x * y;
-  const float r = __builtin_fmaf(-q0, b, x);
-  return __builtin_fmaf(r, y, q0);
 }
 
 __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {

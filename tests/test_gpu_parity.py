@@ -220,6 +220,33 @@ def test_camera_division_equals_ieee(gpu):
     assert bad.size == 0, (bad.size, a[bad[:4]], b[bad[:4]], dev[bad[:4]], ref[bad[:4]])
 
 
+def test_sphere_root_division_equals_ieee(gpu):
+    """cand_sphere_rcp's roots (-hb -+ sq) / a by Markstein's correction from y = RN(1 / a): over the
+    range the kernel takes that path for (a in [2^-60, 2^60], |numerator| < 2^64) the quotient is the
+    IEEE one bit for bit wherever it is normal, and below 2^-126 both are < TMIN (rejected alike)."""
+    rtw = gpu
+    rng = np.random.default_rng(13)
+    n = 1 << 22
+
+    def rand_f32(lo_e, hi_e, signed):
+        e = rng.integers(lo_e, hi_e, n)
+        m = rng.random(n) + 1.0
+        x = (m * np.exp2(e.astype(np.float64))).astype(np.float32)
+        if signed:
+            x = np.where(rng.random(n) < 0.5, -x, x).astype(np.float32)
+        return x
+    num = rand_f32(-70, 64, True)
+    a = rand_f32(-60, 60, False)
+    num[:4096] = 0.0
+    dev = rtw.diag_libm(4, num, a)
+    ref = (num / a).astype(np.float32)
+    normal = np.abs(ref) >= np.float32(2.0 ** -126)
+    bad = np.nonzero(normal & (dev.view(np.uint32) != ref.view(np.uint32)))[0]
+    assert bad.size == 0, (bad.size, num[bad[:4]], a[bad[:4]], dev[bad[:4]], ref[bad[:4]])
+    tiny = ~normal
+    assert np.all(np.abs(dev[tiny]) < 0.001) and np.all(np.abs(ref[tiny]) < 0.001)
+
+
 def test_render_stream_pixels(gpu):
     """Raytracer::render() as a Pixel stream (lib.rs:50-76): same sums as rtw_render, emitted
     row j = h-1 .. 0, column 0 .. w-1, band by band; the ProgressMessage frames round-trip."""
