@@ -259,7 +259,8 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
 
 /* Diagnostics: evaluate the render path's f32 transcendentals on the device over n host values
  * (fn 0 log10f(a), 1 sinf(a), 2 acosf(a), 3 atan2f(a, b); DESIGN.md §Parity: correctly rounded;
- * fn 4 a / b by the camera's Markstein division from the reciprocal RN(1 / b)).
+ * fn 4 a / b by the camera's Markstein division from the reciprocal RN(1 / b), fn 5 the sphere
+ * test's sqrt(a)).
  * Used by the parity tests to pin the device functions against the oracle's. */
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
 

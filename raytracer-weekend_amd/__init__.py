@@ -524,7 +524,8 @@ def unpack_tiles_device(w, h, d_tiles_ptr, n_tiles, d_packed_ptr, d_image_ptr, d
 
 def diag_libm(fn: int, a, b=None) -> np.ndarray:
     """Device f32 transcendentals (0 log10f, 1 sinf, 2 acosf, 3 atan2f(a, b)) and the camera's
-    division (4: a / b by Markstein's correction from RN(1 / b)) over host arrays."""
+    division (4: a / b by Markstein's correction from RN(1 / b)) and the sphere test's sqrt (5) over
+    host arrays."""
     a = _fa(a)
     bb = _fa(b) if b is not None else None
     out = np.empty_like(a)

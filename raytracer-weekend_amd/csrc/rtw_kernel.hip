@@ -66,6 +66,22 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// Correctly rounded f32 sqrt for x in [2^-96, inf): the backend's own expansion of sqrtf (v_sqrt_f32,
+// then the +-1 ulp residual corrections) without its small-input scaling and special-value fix-up,
+// which select the unscaled, uncorrected result for exactly these inputs -- the same bits, 7 fewer
+// VALU ops.  tests/test_gpu_parity.py checks it against IEEE sqrt on the device.
+__device__ __forceinline__ float sqrt_rn_big(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+  const float s1 = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+  return __builtin_fmaf(-sup, s, x) > 0.0f ? sup : s1;
+}
+__device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
+  float r = sqrt_rn_big(x);
+  if (__builtin_expect(!(x >= 0x1p-96f && x < INFINITY), 0)) r = sqrtf(x);
+  return r;
+}
 __device__ __forceinline__ V3 unit(V3 a) { return divs(a, sqrtf(len2(a))); }       // vec3.rs:85-87
 __device__ __forceinline__ bool near_zero(V3 a) {                                   // vec3.rs:133-138
   return fabsf(a.x) < 1e-8f && fabsf(a.y) < 1e-8f && fabsf(a.z) < 1e-8f;
@@ -320,7 +336,7 @@ __device__ __forceinline__ float cand_sphere_rcp(const Ray& r, V3 c, float rad2,
   float cc = len2(oc) - rad2;
   float disc = hb * hb - q.a * cc;
   if (!(disc >= 0.0f)) return -1.0f;
-  float sq = sqrtf(disc);
+  float sq = sqrt_rn(disc);
   float root = sph_div(-hb - sq, q);
   if (root < TMIN) root = sph_div(-hb + sq, q);
   return root;
@@ -1330,6 +1346,10 @@ __global__ void libm_kernel(int fn, uint32_t n, const float* a, const float* b, 
     out[g] = div_by_recip(x, b[g], 1.0f / b[g]);
     return;
   }
+  if (fn == 5) {  // the sphere test's sqrt
+    out[g] = sqrt_rn(x);
+    return;
+  }
   out[g] = fn == 0 ? dev_log10f(x) : (fn == 1 ? dev_sinf(x) : (fn == 2 ? dev_acosf(x) : dev_atan2f(x, b[g])));
 }
 
@@ -1875,7 +1895,7 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
 }
 
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out) {
-  if (fn < 0 || fn > 4 || (n && (!a || !out || (fn >= 3 && !b)))) return fail(RTW_EINVAL, "bad arguments");
+  if (fn < 0 || fn > 5 || (n && (!a || !out || ((fn == 3 || fn == 4) && !b)))) return fail(RTW_EINVAL, "bad arguments");
   if (!n) return RTW_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
@@ -1883,7 +1903,7 @@ int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out
   const size_t bytes = (size_t)n * sizeof(float);
   int rc = RTW_OK;
   if (hipMalloc((void**)&da, bytes) != hipSuccess || hipMalloc((void**)&dout, bytes) != hipSuccess ||
-      (fn >= 3 && hipMalloc((void**)&db, bytes) != hipSuccess)) {
+      ((fn == 3 || fn == 4) && hipMalloc((void**)&db, bytes) != hipSuccess)) {
     rc = fail(RTW_ENOMEM, "hipMalloc(diag)");
   } else if (hipMemcpy(da, a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
              (db && hipMemcpy(db, b, bytes, hipMemcpyHostToDevice) != hipSuccess)) {

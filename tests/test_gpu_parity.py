@@ -247,6 +247,25 @@ def test_sphere_root_division_equals_ieee(gpu):
     assert np.all(np.abs(dev[tiny]) < 0.001) and np.all(np.abs(ref[tiny]) < 0.001)
 
 
+def test_sphere_sqrt_equals_ieee(gpu):
+    """The sphere test's sqrt (sqrt_rn: the backend's correctly rounded expansion without the scaling
+    it only applies below 2^-96) equals IEEE sqrt: every mantissa at an even and an odd exponent, the
+    2^-96 boundary, zeros, subnormals, infinities and NaN, and random floats over the whole range."""
+    rtw = gpu
+    m = np.arange(1 << 23, dtype=np.uint32)
+    x = np.concatenate([(m | np.uint32(127 << 23)), (m | np.uint32(128 << 23)),
+                        np.arange(0x0F800000 - 4096, 0x0F800000 + 4096, dtype=np.uint32),  # 2^-96
+                        np.arange(0, 1 << 16, dtype=np.uint32),                              # subnormals
+                        np.array([0x7F7FFFFF, 0x7F800000, 0x7FC00000, 0x80000000, 0xBF800000], np.uint32),
+                        np.random.default_rng(17).integers(0, 0x7F800000, 1 << 22, dtype=np.uint32)]).view(np.float32)
+    dev = rtw.diag_libm(5, x)
+    with np.errstate(invalid="ignore"):
+        ref = np.sqrt(x)
+    same = (dev.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(dev) & np.isnan(ref))
+    bad = np.nonzero(~same)[0]
+    assert bad.size == 0, (bad.size, x[bad[:4]], dev[bad[:4]], ref[bad[:4]])
+
+
 def test_render_stream_pixels(gpu):
     """Raytracer::render() as a Pixel stream (lib.rs:50-76): same sums as rtw_render, emitted
     row j = h-1 .. 0, column 0 .. w-1, band by band; the ProgressMessage frames round-trip."""
