@@ -263,6 +263,9 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
  * test's sqrt(a)).
  * Used by the parity tests to pin the device functions against the oracle's. */
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
+/* Diagnostics (host only, no device): the host's RN(1 / b) that the camera's u, v divisions use
+ * (rtw_render*: b = w - 1, h - 1), over n values; exact for integer-valued b in [1, 2^24). */
+int rtw_diag_recip(uint32_t n, const float* b, float* out);
 
 /* console_app/src/main.rs:68-90 tonemap: sqrt(sum/spp), clamp [0, 0.999], u8(255.999*c). */
 int rtw_tonemap(const float* rgb_sum, uint32_t n_pixels, uint32_t spp, uint8_t* rgb8);

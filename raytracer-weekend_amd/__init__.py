@@ -134,6 +134,7 @@ _SIGS = {
                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
     "rtw_diag_libm": (C.c_int, [C.c_int, C.c_uint32, _F, _F, _F]),
+    "rtw_diag_recip": (C.c_int, [C.c_uint32, _F, _F]),
     "rtw_scene_preset": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_uint64, C.c_char_p,
                                    C.POINTER(rtw_camera), _F]),
     "rtw_preset_cameras": (C.c_int, [C.c_char_p, C.c_float, C.c_char_p, C.POINTER(rtw_camera), C.c_uint32,
@@ -530,6 +531,14 @@ def diag_libm(fn: int, a, b=None) -> np.ndarray:
     bb = _fa(b) if b is not None else None
     out = np.empty_like(a)
     _check(lib().rtw_diag_libm(fn, len(a), _fp(a), _fp(bb) if bb is not None else None, _fp(out)))
+    return out
+
+
+def diag_recip(b) -> np.ndarray:
+    """The host's RN(1 / b) behind the camera divisions (no device needed)."""
+    b = _fa(b)
+    out = np.empty_like(b)
+    _check(lib().rtw_diag_recip(len(b), _fp(b), _fp(out)))
     return out
 
 

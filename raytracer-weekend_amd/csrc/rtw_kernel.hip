@@ -1894,6 +1894,12 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
   return rc;
 }
 
+int rtw_diag_recip(uint32_t n, const float* b, float* out) {
+  if (n && (!b || !out)) return fail(RTW_EINVAL, "NULL argument");
+  for (uint32_t k = 0; k < n; ++k) out[k] = recip_rn(b[k]);
+  return RTW_OK;
+}
+
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out) {
   if (fn < 0 || fn > 5 || (n && (!a || !out || ((fn == 3 || fn == 4) && !b)))) return fail(RTW_EINVAL, "bad arguments");
   if (!n) return RTW_OK;

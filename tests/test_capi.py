@@ -184,3 +184,13 @@ def test_bvh4_breadth_first_codes_and_bounds(rtw, name):
         inner = [int(nd["child"][i, k]) for k in ch if nd["child"][i, k] >= 0]
         return max(4, len(ch) - 1 + max(bound4(j) for j in inner)) if inner else 4
     assert s.info(11) == bound4(0) >= s.info(8)
+
+
+def test_camera_reciprocal_is_correctly_rounded(rtw):
+    """rtw_render's camera divisions (lib.rs:84-85) use Markstein's correction from the host's
+    RN(1 / (w - 1)) and RN(1 / (h - 1)) (rtw_kernel.hip recip_rn): it must be the IEEE f32 reciprocal
+    for every image size (w, h <= 65536) and beyond, up to 2^24."""
+    b = np.concatenate([np.arange(1, 65536), np.arange(65536, 1 << 24, 4099), [(1 << 24) - 1]]).astype(np.float32)
+    got = rtw.diag_recip(b)
+    want = (np.float32(1.0) / b).astype(np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
