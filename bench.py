@@ -25,14 +25,19 @@ peak.  Reported beside it: the measured HBM fraction (rocprofv3 PMC bytes per la
 cache-level algorithmic bytes.  scripts/roofline.py recomputes all of them from profiles/.
 
 `cpu_baseline` is the oracle (the reference algorithm restated in C, flat-list closest hit,
-recursive sample_ray; -O3) on every host core of the box, best of 3 over a bounded row sample
+recursive sample_ray; -O3) on the host CPUs this process may use (the cgroup CPU quota when there
+is one, else every logical CPU; `cores` states that number), best of 3 over a bounded row sample
 of the same frame, rank 0 at N=1 only.
+
+N > 1 prints, beside `value`, the per-rank path-kernel ms, the all-gather ms and the max/min
+imbalance across ranks (`multi_gpu`), so a scaling run separates load imbalance from gather cost.
 """
 from __future__ import annotations
 
 import argparse
 import importlib.util
 import json
+import math
 import os
 import sys
 import time
@@ -104,7 +109,11 @@ def cpu_baseline(scene, cam, bg, w, h, spp, budget_s: float) -> dict:
     orc = _load("rtw_oracle_py", ROOT / "oracle" / "oracle.py")
     o = orc.OracleScene(scene.dump(), scene.images())
     ocam = orc.camera_from_fields(cam.as_dict())
-    threads = min(256, os.cpu_count() or 1)  # oracle_render's thread cap
+    nproc = os.cpu_count() or 1
+    quota = cpu_quota()
+    # one thread per CPU the cgroup grants (a 16-CPU quota on a 256-thread EPYC: 16 threads), the
+    # Rayon pool's size on that box (lib.rs:60-67 runs over the cores it has); oracle_render caps at 256
+    threads = max(1, min(256, nproc, math.ceil(quota) if quota else nproc))
     spp_s = max(1, min(spp, 8))
     order = list(range(0, h, 37)) + [j for j in range(h) if j % 37]  # strided first
 
@@ -123,9 +132,11 @@ def cpu_baseline(scene, cam, bg, w, h, spp, budget_s: float) -> dict:
         dt, rays = run(rows)
         times.append(dt)
     best = min(times)
+    where = (f"cgroup quota of {quota:g} CPUs on a {nproc}-thread {cpu_model()}" if quota
+             else f"all {nproc} logical CPUs of a {cpu_model()}")
     return {"value": round(rays / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "cpu_quota_cores": cpu_quota(), "nproc": os.cpu_count(),
-            "label": f"CPU restatement, {threads} threads; baseline only",
+            "cpu_quota_cores": quota, "nproc": nproc,
+            "label": f"CPU restatement, {threads} cores ({where}); baseline only",
             "sample": f"{len(rows)} of {h} rows x {w} px x {spp_s} spp of the same frame, best of 3 "
                       f"({rays} rays in {best:.2f} s; runs {', '.join(f'{t:.2f}' for t in times)} s), "
                       f"oracle/rtw_oracle.c -O3, {threads} threads, CPU {cpu_model()}"}
@@ -242,6 +253,9 @@ def main() -> int:
         if world == 1 and launches == 1:  # one GPU: the whole frame straight into the image (rtw_render's path)
             rt.render_device(image.data_ptr(), dev, 0, 0, stream.cuda_stream)
             return
+        if launches == 1:  # this rank's tiles rank, rank + world, ... (the kernel computes them: no id table)
+            rt.render_device_strided(packed.data_ptr(), dev, rank, world, n_mine, stream.cuda_stream)
+            return
         for k in range(launches):
             a, b = int(bounds[k]), int(bounds[k + 1])
             rt.render_device(packed[a:].data_ptr(), dev, ids[a:].data_ptr(), b - a, stream.cuda_stream)
@@ -250,14 +264,24 @@ def main() -> int:
         if multi:
             return
         if world > 1 and args.backend == "gloo":  # CPU rehearsal: gather through host memory
+            if gev is not None:
+                gev[0].record(stream)
             g = torch.zeros(gathered.shape, dtype=torch.float32)
             dist.all_gather_into_tensor(g, packed.cpu())
             gathered.copy_(g)
+            if gev is not None:
+                gev[1].record(stream)
+                gather_ev.append(gev)
             if rank == 0:
                 rtw.unpack_tiles_device(w, h, all_ids.data_ptr(), world * per_rank, gathered.data_ptr(),
                                         image.data_ptr(), dev, stream.cuda_stream)
         elif world > 1:
+            if gev is not None:
+                gev[0].record(stream)
             dist.all_gather_into_tensor(gathered, packed)
+            if gev is not None:  # on torch's stream after the collective: includes waiting for the slowest rank
+                gev[1].record(stream)
+                gather_ev.append(gev)
             if rank == 0:
                 rtw.unpack_tiles_device(w, h, all_ids.data_ptr(), world * per_rank, gathered.data_ptr(),
                                         image.data_ptr(), dev, stream.cuda_stream)
@@ -267,12 +291,18 @@ def main() -> int:
         if rank == 0:
             host_image.copy_(image, non_blocking=True)
 
+    gev = None         # (start, end) events of the current step's all-gather (N > 1)
+    gather_ev = []     # those of the timed steps
     # exact ray count + traversal counters of this rank's share (untimed, same seed => same work)
     st = rt.render_device(packed.data_ptr(), dev, ids.data_ptr(), n_mine, stream.cuda_stream,
                           flags=rtw.FLAG_COUNT_TRAVERSAL, want_stats=True)
     counts = torch.tensor([st["rays"], st["node_visits"], st["boxes_tested"], n_mine * 64 * spp]
                           + st["prim_tests_by_type"], dtype=torch.float64, device=dev)
+    rank_rays = [int(st["rays"])]
     if world > 1:
+        rr = [torch.zeros_like(counts) for _ in range(world)]
+        dist.all_gather(rr, counts)
+        rank_rays = [int(x[0].item()) for x in rr]
         dist.all_reduce(counts)
     counts = counts.cpu().numpy()
     frame_rays = int(counts[0])
@@ -306,6 +336,8 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if world > 1:
+            gev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         render_frame()
         frame_end()
     torch.cuda.synchronize()
@@ -319,6 +351,9 @@ def main() -> int:
         dt = float(t.item())
     # path_kernel alone: the library's HIP events around each launch on the launch stream, all K
     # steps (a render call splits a frame larger than 2^32 paths into several passes, one launch each)
+    # every frame rendered so far is valid: no traversal guard tripped (raises otherwise)
+    for d in (range(multi) if multi else [dev]):
+        scene.render_status(d)
     pk = scene.path_kernel_times(0 if multi else dev)
     if not pk or len(pk) >= 64 or len(pk) % (args.steps * launches):
         raise SystemExit(f"path-kernel timings: got {len(pk)} for {args.steps} steps x {launches} calls "
@@ -343,6 +378,19 @@ def main() -> int:
         issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit",
                                         "ta_busy", "td_busy", "lds_active", "lds_conflict_share")}
         issue["source"] = str(vj.relative_to(ROOT))
+    multi_gpu = None
+    if world > 1:  # per-rank kernel / gather time: imbalance vs gather cost (a scaling run's diagnosis)
+        gms = sum(a.elapsed_time(b) for a, b in gather_ev) / len(gather_ev) if gather_ev else float("nan")
+        mine_t = torch.tensor([frame_kernel_ms, gms], dtype=torch.float64, device=dev)
+        allt = [torch.zeros_like(mine_t) for _ in range(world)]
+        dist.all_gather(allt, mine_t)
+        km = [round(float(x[0].item()), 3) for x in allt]
+        gm = [round(float(x[1].item()), 3) for x in allt]
+        multi_gpu = {"rank_kernel_ms_per_frame": km, "rank_gather_ms_per_frame": gm, "rank_rays_per_frame": rank_rays,
+                     "kernel_imbalance_max_over_min": round(max(km) / min(km), 4) if min(km) > 0 else None,
+                     "gather_ms_min_over_ranks": min(gm),
+                     "note": "gather ms = all-gather on torch's stream, incl. waiting for the slowest rank; its "
+                             "minimum over ranks (the slowest rank's) is the transfer cost"}
     n_launch = launches * passes
     # per launch of this rank (multi-device: device 0's launches, its 1/N share of the frame)
     roof = roofline(cnt, frame_kernel_ms / n_launch, n_launch, multi or world, traffic, issue)
@@ -380,6 +428,8 @@ def main() -> int:
             "roofline": roof,
             "paths_per_sec": round(w * h * spp * args.steps / dt, 1),
         }
+        if multi_gpu:
+            out["multi_gpu"] = multi_gpu
         if n_dev == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, cam, bg, w, h, spp, args.cpu_budget)
         else:

@@ -221,11 +221,30 @@ int rtw_progress_decode(const uint8_t* frame, size_t len, rtw_progress_msg* msg)
  * path queue and one sample buffer: renders of a scene on one device must be serialised on one
  * stream (two renders in flight on different streams would share them).  The first render of a
  * given size allocates the sample buffer (hipMalloc: not stream-capturable); later renders of the
- * same or a smaller size only enqueue. */
+ * same or a smaller size only enqueue.  Without stats, a traversal fault of this render surfaces at
+ * the next call (rtw_render_status). */
 int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float background[3],
                       uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
                       const uint32_t* d_tile_ids, uint32_t n_tiles, float* d_out, void* stream,
                       uint32_t flags, rtw_stats* stats);
+/* rtw_render_device over the tiles first_tile + k * tile_stride (k < n_tiles) without an id table
+ * (the kernel computes them): a device's round-robin share of the frame (rtw_tile_partition part p of
+ * n: first_tile = p, tile_stride = n).  d_out is packed [n_tiles][64][3].  RTW_EINVAL if a tile
+ * leaves the frame or tile_stride == 0. */
+int rtw_render_device_strided(rtw_scene* s, int device, const rtw_camera* cam, const float background[3],
+                              uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
+                              uint32_t first_tile, uint32_t tile_stride, uint32_t n_tiles, float* d_out,
+                              void* stream, uint32_t flags, rtw_stats* stats);
+/* Errors of renders the caller did not wait for.  A path kernel whose BVH walk trips its guard (a
+ * corrupt tree: the walk is bounded so every wave drains) sets the device's host-mapped error word.
+ * It is reported, and cleared, as RTW_EINVAL by the next rtw_render* call on that device (before it
+ * enqueues), by rtw_path_kernel_times, by any call with stats, and by this function, which first
+ * waits for all work on the device (hipDeviceSynchronize).  RTW_OK = every frame rendered so far on
+ * `device` (-1: the first copy) is valid. */
+int rtw_render_status(rtw_scene* s, int device);
+/* Test hook: overwrite the device copy's first two BVH nodes with a cycle, so that every render of it
+ * trips the traversal guard (tests/test_gpu_parity.py).  The scene stays unusable on that device. */
+int rtw_diag_corrupt_bvh(rtw_scene* s, int device);
 
 /* Raytracer::new(..).render().collect() (lib.rs:40-95) over n_gpus devices of this node, driven from
  * the calling host thread (the reference's Rayon pixel parallelism, lib.rs:57-76, becomes tiles
@@ -235,7 +254,9 @@ int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const flo
  * use) brings the tiles to device 0, which assembles the frame and copies it into out_rgb_sum in the
  * same layout as rtw_render.  n_gpus <= 0 = every visible device.  The frame is bit-identical to
  * rtw_render's for every n_gpus (per-pixel random streams).  stats->rays sums the devices,
- * stats->kernel_ms is the slowest device's.  Blocking. */
+ * stats->kernel_ms is the slowest device's.  Blocking.  With one device (n_gpus = 1, or 0 on a one-GPU
+ * node) it is rtw_render's path on device 0 and never opens RCCL; RTW_RCCL_LIB names another RCCL
+ * library to open. */
 int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const float background[3], uint32_t w,
                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, float* out_rgb_sum,
                      rtw_stats* stats);
@@ -253,7 +274,8 @@ int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* 
 
 /* Device time (ms, HIP events on the render stream) of the most recent path-kernel launches of
  * rtw_render / rtw_render_device on `device`, oldest first: at most max_n of the last 64, written
- * to ms[]; returns how many (>= 0) or an error, and forgets them.  Waits for those launches.
+ * to ms[]; returns how many (>= 0) or an error, and forgets them.  Waits for those launches, and
+ * returns RTW_EINVAL if one of them tripped the traversal guard (rtw_render_status).
  * (Benchmark hook: the render call itself also enqueues the in-order sample reduction.) */
 int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
 

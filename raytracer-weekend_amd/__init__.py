@@ -121,6 +121,11 @@ _SIGS = {
     "rtw_render_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_uint32, C.c_uint64, _U32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
+    "rtw_render_device_strided": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32,
+                                            C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                            C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
+    "rtw_render_status": (C.c_int, [C.c_void_p, C.c_int]),
+    "rtw_diag_corrupt_bvh": (C.c_int, [C.c_void_p, C.c_int]),
     "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
     "rtw_render_multi": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.c_uint32, C.c_uint64, _F, C.POINTER(rtw_stats)]),
@@ -398,6 +403,14 @@ class Scene:
             _check(n)
         return [float(buf[q]) for q in range(n)]
 
+    def render_status(self, device: int = -1) -> None:
+        """Wait for the device and raise if a render since the last check tripped the traversal guard."""
+        _check(lib().rtw_render_status(self._p, device))
+
+    def diag_corrupt_bvh(self, device: int = -1) -> None:
+        """Test hook: a cyclic BVH on the device copy (every render of it trips the guard)."""
+        _check(lib().rtw_diag_corrupt_bvh(self._p, device))
+
     def info(self, what: int) -> int:
         return int(lib().rtw_scene_info(self._p, what))
 
@@ -472,6 +485,17 @@ class Raytracer:
             self.scene._p, device, C.byref(self.cam.c), _fp(self.bg), self.w, self.h, self.spp, self.max_depth,
             self.seed, C.cast(C.c_void_p(d_tiles_ptr), _U32) if d_tiles_ptr else None, n_tiles,
             C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr), flags, C.byref(st) if want_stats else None))
+        return st.as_dict() if want_stats else None
+
+    def render_device_strided(self, d_out_ptr: int, device: int, first_tile: int, tile_stride: int, n_tiles: int,
+                              stream_ptr: int = 0, flags: int = 0, want_stats: bool = False):
+        """Enqueue tiles first_tile + k * tile_stride (k < n_tiles) into packed device memory
+        [n_tiles][64][3] (a device's round-robin share of the frame, no id table)."""
+        st = rtw_stats()
+        _check(lib().rtw_render_device_strided(
+            self.scene._p, device, C.byref(self.cam.c), _fp(self.bg), self.w, self.h, self.spp, self.max_depth,
+            self.seed, first_tile, tile_stride, n_tiles, C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr), flags,
+            C.byref(st) if want_stats else None))
         return st.as_dict() if want_stats else None
 
 

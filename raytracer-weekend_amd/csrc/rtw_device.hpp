@@ -190,13 +190,16 @@ struct RenderArgs {
   float rw1, rh1;             // RN(1 / fw1), RN(1 / fh1): the camera divisions by Markstein's correction
   float time_span;            // cam.time1 - cam.time0 in f32 (UniformFloat scale, camera.rs:72)
   uint64_t tiles_x_magic;     // UINT64_MAX / tiles_x + 1 (tiles_x >= 2)
-  const uint32_t* tile_ids;   // device array or nullptr (slot == tile id, full-image output)
+  const uint32_t* tile_ids;   // device array, or nullptr: slot s renders tile tile_first + s * tile_stride
+  uint32_t tile_first, tile_stride;  // (a device's round-robin share of the frame without an id table)
+  uint32_t packed_out;        // output [slot][64][3] (always with tile_ids); else the full w x h image
   uint64_t seed_hash;         // splitmix64(seed)
   uint64_t n_paths;           // paths in this pass = slots * 64 * spp
   float* sbuf;                // ordered sample buffer: n_paths x (r, g, b) floats, path-major
   float* out;
-  unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type, [30] error flag
+  unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
   unsigned long long* queue;     // path-id dispenser of this pass
+  uint32_t* err;                 // host-mapped sticky error word: 1 = a traversal guard tripped (DeviceCopy::err_host)
   int32_t* spill;                // traversal stack entries beyond the LDS stack: [depth][lane]
   uint32_t spill_depth;          // entries per lane (0 = the LDS stack covers the tree's bound)
   uint32_t spill_lanes;          // resident lanes of the launch (stride between levels)

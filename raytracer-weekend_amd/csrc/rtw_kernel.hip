@@ -617,7 +617,7 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
-                          unsigned long long* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
+                          uint32_t* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
@@ -649,7 +649,8 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
   const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes) : reinterpret_cast<const char*>(S.nodes);
   // every wave must drain: a corrupt tree (a cycle) ends the walk instead of hanging the GPU, and
-  // raises the launch's error flag (counters[30]), which the host turns into RTW_EINVAL
+  // sets the device's host-mapped error word (RenderArgs::err), which the host turns into RTW_EINVAL
+  // at the next render call, rtw_render_status, rtw_path_kernel_times or a stats read
   constexpr uint32_t GUARD = 1u << 20;
   uint32_t guard = 0;
   for (; guard < GUARD; ++guard) {
@@ -819,7 +820,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     const uint64_t done = __ballot(ts.node < 0 && ts.sp == 0);
     if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) return;
   }
-  *err = 1ull;  // a guard tripped: end this traversal (miss) and report
+  *err = 1u;  // a guard tripped: end this traversal (miss) and report (a vector store to host memory)
   ts.node = -1;
   ts.sp = 0;
   ts.pend = 0;
@@ -1078,7 +1079,7 @@ __device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, Pa
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
   const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
   const uint32_t gslot = a.slot_base + slot;
-  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
+  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : a.tile_first + gslot * a.tile_stride;
   const uint32_t ty = a.tiles_x > 1u ? fastdiv(tile, a.tiles_x_magic) : tile;
   const uint32_t i = (tile - ty * a.tiles_x) * 8u + (l & 7u), row = ty * 8u + (l >> 3);
   if (i >= a.w || row >= a.h) return false;
@@ -1202,7 +1203,7 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
-                                                      leaf_thr, st.rng, a.counters + 30, ph + 4, nodes_lds, stk16);
+                                                      leaf_thr, st.rng, a.err, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1311,7 +1312,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_slots * 64u) return;
   const uint32_t slot = g >> 6, l = g & 63u, gslot = a.slot_base + slot;
-  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : gslot;
+  const uint32_t tile = a.tile_ids ? a.tile_ids[gslot] : a.tile_first + gslot * a.tile_stride;
   const uint32_t i = (tile % a.tiles_x) * 8u + (l & 7u), row = (tile / a.tiles_x) * 8u + (l >> 3);
   if (i >= a.w || row >= a.h) return;
   float x = 0.f, y = 0.f, z = 0.f;
@@ -1321,7 +1322,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
     y = y + q[1];
     z = z + q[2];
   }
-  float* o = a.tile_ids ? a.out + ((size_t)gslot * 64u + l) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
+  float* o = a.packed_out ? a.out + ((size_t)gslot * 64u + l) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
   o[0] = x;
   o[1] = y;
   o[2] = z;
@@ -1396,6 +1397,10 @@ int upload(Scene& s, int device) {
     HIPCHK(hipMalloc(&c.block, c.bytes), "hipMalloc(scene)");
     HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
     HIPCHK(hipMalloc((void**)&c.counters, 32 * sizeof(unsigned long long)), "hipMalloc(counters)");
+    // the sticky traversal-error word lives in host memory the kernel writes through (coherent,
+    // mapped): the host reads it without a device round trip, also for renders it did not wait for
+    HIPCHK(hipHostMalloc((void**)&c.err_host, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc(error word)");
+    *(volatile uint32_t*)c.err_host = 0u;
     uint8_t* base = (uint8_t*)c.block;
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
@@ -1431,6 +1436,7 @@ void release(Scene& s) {
     if (hipSetDevice(c.device) != hipSuccess) continue;
     if (c.block) hipFree(c.block);
     if (c.counters) hipFree(c.counters);
+    if (c.err_host) hipHostFree(c.err_host);
     if (c.sbuf) hipFree(c.sbuf);
     if (c.spill) hipFree(c.spill);
     for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids}) free_buf(*b);
@@ -1593,11 +1599,25 @@ static float recip_rn(float b) {
   return best;
 }
 
+int check_guard(DeviceCopy& c) {
+  volatile uint32_t* e = c.err_host;
+  if (e && *e) {
+    *e = 0u;
+    return fail(RTW_EINVAL, "a path kernel on device %d tripped its BVH traversal guard (corrupt tree?): the frame "
+                "it rendered is invalid", c.device);
+  }
+  return RTW_OK;
+}
+
 int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
-                   uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles, uint32_t n_slots,
-                   float* d_out, void* stream_, uint32_t flags, void* ev0_, void* ev1_) {
+                   uint32_t spp, uint32_t max_depth, uint64_t seed, const TileSet& ts, float* d_out, void* stream_,
+                   uint32_t flags, void* ev0_, void* ev1_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   hipEvent_t ev0 = static_cast<hipEvent_t>(ev0_), ev1 = static_cast<hipEvent_t>(ev1_);
+  const uint32_t* d_tiles = ts.ids;
+  const uint32_t n_slots = ts.n;
+  // an earlier render on this device (one the caller did not wait on) tripped the guard: report it now
+  if (int e = check_guard(c)) return e;
   if (w > 65536u || h > 65536u)
     return fail(RTW_EINVAL, "image %ux%u: at most 65536 x 65536 (16-bit pixel coordinates in the path key)", w, h);
   if (cam->time0 < sc.flat.time_lo || cam->time1 > sc.flat.time_hi)
@@ -1629,6 +1649,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   }
   a.tiles_x_magic = a.tiles_x > 1u ? UINT64_MAX / a.tiles_x + 1u : 0u;
   a.tile_ids = d_tiles;
+  a.tile_first = ts.first;
+  a.tile_stride = ts.stride;
+  a.packed_out = (d_tiles || ts.packed) ? 1u : 0u;
+  a.err = c.err_host;
   a.batch = (uint32_t)std::min(65536, std::max(64, env_int("RTW_BATCH", (int)dev::BATCH)));
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
   if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
@@ -1646,7 +1670,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   HIPCHK(hipMemsetAsync(c.counters, 0, 32 * sizeof(unsigned long long), stream), "hipMemsetAsync");
   if (ev0) HIPCHK(hipEventRecord(ev0, stream), "hipEventRecord");
   if (n_slots && (spp == 0 || max_depth == 0)) {  // lib.rs:83 loops 0 times / :98 returns black
-    size_t n = d_tiles ? (size_t)n_slots * 64 * 3 : (size_t)w * h * 3;
+    size_t n = a.packed_out ? (size_t)n_slots * 64 * 3 : (size_t)w * h * 3;
     HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
   } else if (n_slots) {
     const uint64_t per_slot = 64ull * spp;
@@ -1675,8 +1699,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
     a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
     const int grid = resident_grid(c, fn, var.block, count);
+    // the LDS-node variants walk 16-bit codes within their own stack rows (pick_kernel checked
+    // stack_need4 against them) and have no HBM spill path
     const uint32_t lds = var.stack;
-    a.spill_depth = sc.flat.stack_need > lds ? sc.flat.stack_need - lds : 0;
+    a.spill_depth = (!var.k16 && sc.flat.stack_need > lds) ? sc.flat.stack_need - lds : 0;
     a.spill_lanes = (uint32_t)grid * var.block;
     const size_t spill_bytes = (size_t)a.spill_depth * a.spill_lanes * sizeof(int32_t);
     if (spill_bytes > c.spill_bytes) {  // first render of a deep tree only
@@ -1716,7 +1742,7 @@ int collect_stats(DeviceCopy& c, void* stream_, void* ev0_, void* ev1_, uint64_t
   HIPCHK(hipMemcpy(cnt, c.counters, sizeof cnt, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
   float ms = 0.f;
   if (ev0 && ev1) HIPCHK(hipEventElapsedTime(&ms, ev0, ev1), "hipEventElapsedTime");
-  if (cnt[30]) return fail(RTW_EINVAL, "BVH traversal guard tripped (corrupt tree?): the frame is invalid");
+  if (int e = check_guard(c)) return e;
   st->rays = cnt[0];
   st->paths = paths;
   st->kernel_ms = ms;
@@ -1777,7 +1803,9 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t 
   const uint32_t n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
   rtw_stats st;
   memset(&st, 0, sizeof st);
-  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, nullptr, n_tiles, d_out, nullptr, 0, e0, e1);
+  TileSet all;
+  all.n = n_tiles;
+  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, all, d_out, nullptr, 0, e0, e1);
   if (rc == RTW_OK) rc = collect_stats(*c, nullptr, e0, e1, (uint64_t)w * h * spp, &st);
   if (rc == RTW_OK && hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(RTW_ENODEV, "hipMemcpy(image)");
@@ -1786,30 +1814,90 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t 
   return rc;
 }
 
-int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w,
-                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
-                      uint32_t n_tiles, float* d_out, void* stream, uint32_t flags, rtw_stats* stats) {
+static int render_device(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
+                         uint32_t spp, uint32_t max_depth, uint64_t seed, TileSet ts, float* d_out, void* stream,
+                         uint32_t flags, rtw_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!s || !cam || !bg || !d_out) return fail(RTW_EINVAL, "NULL argument");
   if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
   if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2");
   DeviceCopy* c = find_copy(s->s, device);
   if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
-  if (!d_tiles) n_tiles = ((w + 7u) / 8u) * ((h + 7u) / 8u);
   DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (stats)
     if (int e = copy_events(*c, e0, e1)) return e;
-  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_tiles, n_tiles, d_out, stream, flags, e0, e1);
+  int rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, ts, d_out, stream, flags, e0, e1);
   if (rc == RTW_OK && stats) {
     rtw_stats st;
     memset(&st, 0, sizeof st);
-    rc = collect_stats(*c, stream, e0, e1, (uint64_t)n_tiles * 64u * spp, &st);
+    rc = collect_stats(*c, stream, e0, e1, (uint64_t)ts.n * 64u * spp, &st);
     st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *stats = st;
   }
   return rc;
+}
+
+int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w,
+                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles,
+                      uint32_t n_tiles, float* d_out, void* stream, uint32_t flags, rtw_stats* stats) {
+  TileSet ts;
+  ts.ids = d_tiles;
+  ts.n = d_tiles ? n_tiles : ((w + 7u) / 8u) * ((h + 7u) / 8u);
+  return render_device(s, device, cam, bg, w, h, spp, max_depth, seed, ts, d_out, stream, flags, stats);
+}
+
+int rtw_render_device_strided(rtw_scene* s, int device, const rtw_camera* cam, const float bg[3], uint32_t w,
+                              uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, uint32_t first_tile,
+                              uint32_t tile_stride, uint32_t n_tiles, float* d_out, void* stream, uint32_t flags,
+                              rtw_stats* stats) {
+  const uint64_t nt = (uint64_t)((w + 7u) / 8u) * ((h + 7u) / 8u);
+  if (tile_stride == 0 || (n_tiles && first_tile + (uint64_t)(n_tiles - 1) * tile_stride >= nt))
+    return fail(RTW_EINVAL, "tiles %u + k * %u (k < %u) leave the frame's %llu tiles", first_tile, tile_stride, n_tiles,
+                (unsigned long long)nt);
+  TileSet ts;
+  ts.first = first_tile;
+  ts.stride = tile_stride;
+  ts.n = n_tiles;
+  ts.packed = true;
+  return render_device(s, device, cam, bg, w, h, spp, max_depth, seed, ts, d_out, stream, flags, stats);
+}
+
+int rtw_render_status(rtw_scene* s, int device) {
+  if (!s) return fail(RTW_EINVAL, "NULL argument");
+  DeviceCopy* c = find_copy(s->s, device);
+  if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
+  DeviceGuard g;
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipDeviceSynchronize(), "render (hipDeviceSynchronize)");
+  return check_guard(*c);
+}
+
+// Test hook: overwrite the first two node4s of the device copy with a cycle (node 0 -> node 1 -> node 1
+// ..., every box infinite, in both the 32-bit child words and the 16-bit codes), so that every ray's
+// walk trips the traversal guard.  The host tables are untouched; renders of this copy are invalid.
+int rtw_diag_corrupt_bvh(rtw_scene* s, int device) {
+  if (!s) return fail(RTW_EINVAL, "NULL argument");
+  if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
+  DeviceCopy* c = find_copy(s->s, device);
+  if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
+  if (c->scene.n_nodes < 2) return fail(RTW_EINVAL, "the scene's BVH has %u node4s (needs 2)", c->scene.n_nodes);
+  DevNode4 nd[2];
+  memset(nd, 0, sizeof nd);
+  for (DevNode4& n : nd) {
+    for (int k = 0; k < 4; ++k) {
+      const float lo = k ? INFINITY : -1e30f, hi = k ? -INFINITY : 1e30f;  // slots 1-3 empty
+      n.lo_x[k] = n.lo_y[k] = n.lo_z[k] = lo;
+      n.hi_x[k] = n.hi_y[k] = n.hi_z[k] = hi;
+    }
+    n.child[0] = 1;
+    n.code[0] = 1u;
+  }
+  DeviceGuard g;
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipMemcpy(const_cast<DevNode4*>(c->scene.nodes), nd, sizeof nd, hipMemcpyHostToDevice), "hipMemcpy(nodes)");
+  return RTW_OK;
 }
 
 int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h, uint32_t spp,
@@ -1825,26 +1913,23 @@ int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], ui
   const uint32_t band_ty = std::max(1u, ((band_rows ? band_rows : 64u) + 7u) / 8u);  // tile rows per band
   DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  std::vector<uint32_t> ids((size_t)tiles_x * tiles_y);
-  for (uint32_t k = 0; k < ids.size(); ++k) ids[k] = k;  // tile row ty = output rows [8 ty, 8 ty + 8)
   const size_t band_tiles = (size_t)band_ty * tiles_x;
-  if (int e = grow(c->tiles, ids.size() * sizeof(uint32_t))) return e;
   if (int e = grow(c->packed, band_tiles * 64 * 3 * sizeof(float))) return e;
-  uint32_t* d_ids = static_cast<uint32_t*>(c->tiles.p);
   float* d_packed = static_cast<float*>(c->packed.p);
   hipEvent_t e0, e1;
   if (int e = copy_events(*c, e0, e1)) return e;
   int rc = RTW_OK;
-  if (hipMemcpy(d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
-    rc = fail(RTW_ENODEV, "hipMemcpy(tile ids)");
   std::vector<float> packed(band_tiles * 64 * 3);
   std::vector<rtw_pixel> px;
   rtw_stats tot;
   memset(&tot, 0, sizeof tot);
   for (uint32_t ty0 = 0; rc == RTW_OK && ty0 < tiles_y; ty0 += band_ty) {
     const uint32_t nty = std::min(band_ty, tiles_y - ty0), nt = nty * tiles_x;
-    rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, d_ids + (size_t)ty0 * tiles_x, nt, d_packed,
-                        nullptr, 0, e0, e1);
+    TileSet band;  // tile row ty = output rows [8 ty, 8 ty + 8): the band's tiles are consecutive
+    band.first = ty0 * tiles_x;
+    band.n = nt;
+    band.packed = true;
+    rc = enqueue_render(s->s, *c, cam, bg, w, h, spp, max_depth, seed, band, d_packed, nullptr, 0, e0, e1);
     rtw_stats st;
     memset(&st, 0, sizeof st);
     if (rc == RTW_OK) rc = collect_stats(*c, nullptr, e0, e1, 0, &st);
@@ -1890,6 +1975,8 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
     }
   }
   c->kev_count = 0;
+  if (rc >= 0 && n)  // the launches waited for: report a tripped traversal guard (its frame is invalid)
+    if (int e = check_guard(*c)) rc = e;
   hipSetDevice(prev);
   return rc;
 }

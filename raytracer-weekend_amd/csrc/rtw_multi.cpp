@@ -9,16 +9,21 @@
 // frame and copies it to the host.  Pixels depend only on (seed, j, i, sample), so the frame is
 // bit-identical to rtw_render's for every n_gpus.
 //
-// RCCL is opened at the first multi-device render (dlopen of librccl.so.1), so the rest of the
-// library does not depend on it.
+// RCCL is opened at the first render over more than one device (dlopen of librccl.so.1, or the file
+// named by RTW_RCCL_LIB), so the rest of the library -- rtw_render_multi(n_gpus = 1) included -- does
+// not depend on it.  The loader and the communicator cache are guarded by one mutex: host threads may
+// call rtw_render_multi concurrently on different scenes.
 #include <dlfcn.h>
+#include <stdlib.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
-#include <type_traits>
 #include <chrono>
+#include <memory>
+#include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rtw.h"
@@ -39,13 +44,23 @@ struct Rccl {
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
+std::mutex& rccl_mutex() {
+  static std::mutex m;
+  return m;
+}
+
+// callers hold rccl_mutex()
 Rccl& rccl() {
   static Rccl r;
   if (r.tried) return r;
   r.tried = true;
-  for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
-    r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
-    if (r.h) break;
+  if (const char* lib = getenv("RTW_RCCL_LIB")) {  // knob: another RCCL build (or a missing one, in tests)
+    r.h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+  } else {
+    for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+      r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (r.h) break;
+    }
   }
   if (!r.h) return r;
   auto sym = [&](auto& fn, const char* n) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r.h, n)); };
@@ -63,13 +78,14 @@ Rccl& rccl() {
   return r;
 }
 
-// one communicator clique per device count, kept for the process (ncclCommInitAll is slow)
+// one communicator clique per device count, kept for the process (ncclCommInitAll is slow); each
+// behind its own allocation, so a pointer handed out stays valid when the cache grows
 struct Clique {
   int n = 0;
   std::vector<ncclComm_t> comms;
 };
-std::vector<Clique>& cliques() {
-  static std::vector<Clique> c;
+std::vector<std::unique_ptr<Clique>>& cliques() {  // callers hold rccl_mutex()
+  static std::vector<std::unique_ptr<Clique>> c;
   return c;
 }
 
@@ -85,21 +101,22 @@ std::vector<Clique>& cliques() {
   } while (0)
 
 int get_clique(int n, std::vector<ncclComm_t>** out) {
-  for (Clique& c : cliques())
-    if (c.n == n) {
-      *out = &c.comms;
+  std::lock_guard<std::mutex> lock(rccl_mutex());
+  for (auto& c : cliques())
+    if (c->n == n) {
+      *out = &c->comms;
       return RTW_OK;
     }
   Rccl& r = rccl();
-  if (!r.h) return fail(RTW_ENODEV, "librccl.so.1 not loadable (multi-device gather needs RCCL)");
-  Clique c;
-  c.n = n;
-  c.comms.resize(n);
+  if (!r.h) return fail(RTW_ENODEV, "librccl.so.1 not loadable (a gather over %d devices needs RCCL)", n);
+  auto c = std::make_unique<Clique>();
+  c->n = n;
+  c->comms.resize(n);
   std::vector<int> devs(n);
   for (int d = 0; d < n; ++d) devs[d] = d;
-  NCCLOK(r.comm_init_all(c.comms.data(), n, devs.data()), "ncclCommInitAll");
-  cliques().push_back(c);
-  *out = &cliques().back().comms;
+  NCCLOK(r.comm_init_all(c->comms.data(), n, devs.data()), "ncclCommInitAll");
+  *out = &c->comms;
+  cliques().push_back(std::move(c));
   return RTW_OK;
 }
 
@@ -139,24 +156,12 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
       if (c.device == d) cp[d] = &c;
     if (!cp[d]) return fail(RTW_ENODEV, "scene was not committed to device %d (commit with device = -1)", d);
   }
-  std::vector<ncclComm_t>* comms = nullptr;
-  if (int e = get_clique(n, &comms)) return e;
-  Rccl& r = rccl();
   int prev = 0;
   hipGetDevice(&prev);
   struct Restore {
     int d;
     ~Restore() { hipSetDevice(d); }
   } restore{prev};
-
-  const uint32_t tiles_x = (w + 7u) / 8u, nt = tiles_x * ((h + 7u) / 8u);
-  const uint32_t per = (nt + (uint32_t)n - 1) / (uint32_t)n;  // padded tiles per device
-  const size_t slot_floats = (size_t)per * 64 * 3;
-  std::vector<uint32_t> ids(per), all((size_t)n * per);
-  std::vector<uint32_t> mine(n);
-  for (int d = 0; d < n; ++d) rtw_tile_partition(w, h, (uint32_t)n, (uint32_t)d, all.data() + (size_t)d * per, per, &mine[d]);
-
-  // 1. every device renders its tiles on its own stream (all enqueued before any wait)
   std::vector<hipEvent_t> e0(n), e1(n);
   for (int d = 0; d < n; ++d) {
     DeviceCopy& c = *cp[d];
@@ -174,13 +179,52 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
       }
     e0[d] = static_cast<hipEvent_t>(c.ev[0]);
     e1[d] = static_cast<hipEvent_t>(c.ev[1]);
+  }
+  const uint32_t tiles_x = (w + 7u) / 8u, nt = tiles_x * ((h + 7u) / 8u);
+  const size_t frame_bytes = (size_t)w * h * 3 * sizeof(float);
+
+  if (n == 1) {  // one device: rtw_render's path (the whole frame straight into the image), no RCCL
+    DeviceCopy& c = *cp[0];
+    HIPOK(hipSetDevice(0), "hipSetDevice");
     hipStream_t st = static_cast<hipStream_t>(c.stream);
-    if (int e = grow(c.tiles, per * sizeof(uint32_t))) return e;
+    if (int e = grow(c.image, frame_bytes)) return e;
+    TileSet all;
+    all.n = nt;
+    if (int e = enqueue_render(s->s, c, cam, bg, w, h, spp, max_depth, seed, all, static_cast<float*>(c.image.p), st, 0,
+                               e0[0], e1[0]))
+      return e;
+    rtw_stats st1;
+    memset(&st1, 0, sizeof st1);
+    if (int e = collect_stats(c, st, e0[0], e1[0], (uint64_t)w * h * spp, &st1)) return e;
+    HIPOK(hipMemcpy(out, c.image.p, frame_bytes, hipMemcpyDeviceToHost), "hipMemcpy(image)");
+    st1.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = st1;
+    return RTW_OK;
+  }
+
+  std::vector<ncclComm_t>* comms = nullptr;
+  if (int e = get_clique(n, &comms)) return e;
+  const Rccl& r = rccl();  // loaded by get_clique; never changes afterwards
+  const uint32_t per = (nt + (uint32_t)n - 1) / (uint32_t)n;  // padded tiles per device
+  const size_t slot_floats = (size_t)per * 64 * 3;
+  std::vector<uint32_t> all((size_t)n * per);
+  std::vector<uint32_t> mine(n);
+  for (int d = 0; d < n; ++d) rtw_tile_partition(w, h, (uint32_t)n, (uint32_t)d, all.data() + (size_t)d * per, per, &mine[d]);
+
+  // 1. every device renders its tiles d, d + n, d + 2n, ... (no id table: the kernel computes them) into its
+  // packed buffer on its own stream, all enqueued before any wait
+  for (int d = 0; d < n; ++d) {
+    DeviceCopy& c = *cp[d];
+    HIPOK(hipSetDevice(d), "hipSetDevice");
+    hipStream_t st = static_cast<hipStream_t>(c.stream);
     if (int e = grow(c.packed, slot_floats * sizeof(float))) return e;
-    HIPOK(hipMemcpyAsync(c.tiles.p, all.data() + (size_t)d * per, per * sizeof(uint32_t), hipMemcpyHostToDevice, st),
-          "hipMemcpyAsync(tile ids)");
-    if (int e = enqueue_render(s->s, c, cam, bg, w, h, spp, max_depth, seed, static_cast<uint32_t*>(c.tiles.p), mine[d],
-                               static_cast<float*>(c.packed.p), st, 0, e0[d], e1[d]))
+    TileSet mt;
+    mt.first = (uint32_t)d;
+    mt.stride = (uint32_t)n;
+    mt.n = mine[d];
+    mt.packed = true;
+    if (int e = enqueue_render(s->s, c, cam, bg, w, h, spp, max_depth, seed, mt, static_cast<float*>(c.packed.p), st, 0,
+                               e0[d], e1[d]))
       return e;
   }
   // 2. one RCCL gather to device 0 (each device's send waits for its render on the same stream)

@@ -87,7 +87,10 @@ struct DeviceCopy {
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
-  unsigned long long* counters = nullptr;  // 32 x u64: [0..19] stats, [30] traversal error flag, [31] path queue
+  unsigned long long* counters = nullptr;  // 32 x u64: [0..23] stats, [31] path queue
+  // host-mapped sticky error word (hipHostMalloc): a path kernel whose traversal guard trips writes 1;
+  // the host reads it at the next render call, rtw_render_status, rtw_path_kernel_times and with stats
+  uint32_t* err_host = nullptr;
   float* sbuf = nullptr;                   // ordered per-sample radiance (rgb per path)
   uint64_t sbuf_paths = 0;
   int32_t* spill = nullptr;                // traversal-stack overflow (trees deeper than the LDS stack)
@@ -126,13 +129,23 @@ int upload(Scene& s, int device);
 void release(Scene& s);
 DeviceCopy* find_copy(Scene& s, int device);  // device < 0: the first copy
 int grow(DevBuf& b, size_t bytes);            // current device; contents not kept
+// Which 8x8 tiles a render covers and where they go: slot k renders tile ids[k] (a device array), or
+// tile first + k * stride without one; the output is packed [slot][64][3] when `packed` (always with
+// ids), else the full w x h image.
+struct TileSet {
+  const uint32_t* ids = nullptr;
+  uint32_t first = 0, stride = 1, n = 0;
+  bool packed = false;
+};
 // enqueue one render (path kernel passes + in-order reductions) on `stream` (hipStream_t) of
-// c.device, which must be current; d_tiles == nullptr renders every tile into a full image
+// c.device, which must be current
 int enqueue_render(Scene& s, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
-                   uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* d_tiles, uint32_t n_tiles,
-                   float* d_out, void* stream, uint32_t flags, void* ev0, void* ev1);
+                   uint32_t spp, uint32_t max_depth, uint64_t seed, const TileSet& tiles, float* d_out,
+                   void* stream, uint32_t flags, void* ev0, void* ev1);
 // wait for `stream`, read the launch counters and the ev0 -> ev1 time into st
 int collect_stats(DeviceCopy& c, void* stream, void* ev0, void* ev1, uint64_t paths, rtw_stats* st);
+// RTW_EINVAL (and clears it) if a path kernel on c's device tripped its traversal guard since the last check
+int check_guard(DeviceCopy& c);
 int enqueue_unpack(uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_tiles, const float* d_packed,
                    float* d_image, void* stream);
 

@@ -129,3 +129,36 @@ def test_c_abi_tile_partition_errors(rtw):
         rtw.tile_partition(64, 64, 0, 0)
     with pytest.raises(rtw.RtwError):
         rtw.tile_partition(64, 64, 2, 2)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_gather_layout_more_parts_than_tiles(rtw, n):
+    """A frame of fewer tiles than devices: rtw_tile_partition gives the extra parts no
+    tiles (n_ids = 0) and pads every part to the common size with ids equal to nt, which the unpack
+    (unpack_tiles_kernel's index math) skips, so the gathered buffer still rebuilds the frame."""
+    import importlib
+    tiles = importlib.import_module("rtw_amd.tiles")
+    w, h = 8, 8  # one tile
+    nt = rtw.n_tiles(w, h)
+    assert nt == 1
+    parts = [rtw.tile_partition(w, h, n, p) for p in range(n)]
+    assert [k for _, k in parts] == [1] + [0] * (n - 1)
+    layout = np.concatenate([ids for ids, _ in parts]).astype(np.int64)
+    assert layout.tolist() == [0] + [nt] * (n - 1)
+    gathered = np.full((n, 64, 3), np.nan, np.float32)  # padding slots hold garbage: never read
+    r, c = tiles.tile_pixels(0, w, h)
+    gathered[0] = fake_pixel(r, c)
+    img = unpack(w, h, layout, gathered)
+    rows, cols = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    assert np.array_equal(img, fake_pixel(rows, cols))
+
+
+def test_strided_render_rejects_tiles_outside_the_frame(rtw):
+    """rtw_render_device_strided validates the tile progression before touching a device."""
+    s = rtw.Scene()
+    cam = rtw.Camera.new((0, 0, 5), (0, 0, 0), (0, 1, 0), 40, 1.0, 0.0, 1.0)
+    rt = rtw.Raytracer(s, cam, (0, 0, 0), 16, 16, 1)  # 4 tiles
+    for first, stride, n in ((0, 0, 1), (0, 2, 3), (4, 1, 1)):
+        with pytest.raises(rtw.RtwError) as e:
+            rt.render_device_strided(1, 0, first, stride, n)
+        assert e.value.code == rtw.RTW_EINVAL
