@@ -285,6 +285,11 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n);
  * test's sqrt(a)).
  * Used by the parity tests to pin the device functions against the oracle's. */
 int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out);
+/* Diagnostics: every 32-bit pattern b in [lo, hi] (as a float) through a device fast path, compared bit
+ * for bit with the IEEE operation on the device.  fn 0: the render path's reciprocal rcp_rn (v_rcp_f32 +
+ * one Newton step) vs 1.0f / b, over |b| in [2^-126, 2^126].  counts[0] = mismatches, counts[1] = patterns
+ * outside the fast path's range (skipped); the first min(cap, counts[0]) mismatching patterns go to bad. */
+int rtw_diag_sweep(int fn, uint32_t lo, uint32_t hi, uint64_t* counts, uint32_t* bad, uint32_t cap);
 /* Diagnostics (host only, no device): the host's RN(1 / b) that the camera's u, v divisions use
  * (rtw_render*: b = w - 1, h - 1), over n values; exact for integer-valued b in [1, 2^24). */
 int rtw_diag_recip(uint32_t n, const float* b, float* out);

@@ -140,6 +140,7 @@ _SIGS = {
     "rtw_tonemap": (C.c_int, [_F, C.c_uint32, C.c_uint32, _U8]),
     "rtw_diag_libm": (C.c_int, [C.c_int, C.c_uint32, _F, _F, _F]),
     "rtw_diag_recip": (C.c_int, [C.c_uint32, _F, _F]),
+    "rtw_diag_sweep": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), _U32, C.c_uint32]),
     "rtw_scene_preset": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_uint64, C.c_char_p,
                                    C.POINTER(rtw_camera), _F]),
     "rtw_preset_cameras": (C.c_int, [C.c_char_p, C.c_float, C.c_char_p, C.POINTER(rtw_camera), C.c_uint32,
@@ -556,6 +557,15 @@ def diag_libm(fn: int, a, b=None) -> np.ndarray:
     out = np.empty_like(a)
     _check(lib().rtw_diag_libm(fn, len(a), _fp(a), _fp(bb) if bb is not None else None, _fp(out)))
     return out
+
+
+def diag_sweep(fn: int, lo: int = 0, hi: int = 0xFFFFFFFF, cap: int = 64):
+    """Device fast path vs the IEEE operation over every bit pattern in [lo, hi] (fn 0: reciprocal)
+    -> (mismatches, skipped, first mismatching patterns)."""
+    counts = (C.c_uint64 * 2)()
+    bad = np.zeros(max(1, cap), np.uint32)
+    _check(lib().rtw_diag_sweep(fn, lo, hi, counts, _up(bad), cap))
+    return int(counts[0]), int(counts[1]), bad[:min(cap, int(counts[0]))]
 
 
 def diag_recip(b) -> np.ndarray:

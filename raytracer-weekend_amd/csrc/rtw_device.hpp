@@ -27,9 +27,9 @@ enum PrimType : uint32_t {
 };
 
 struct alignas(16) DevPrim {
-  // sphere : q0 = (cx, cy, cz, r*r), q1 = (0, 0, 0, key bits), q2 = (0, 1, r, -): a moving sphere
+  // sphere : q0 = (cx, cy, cz, r*r), q1 = (0, 0, 0, key bits), q2 = (0, 1, r, RN(1/r)): a moving sphere
   //          that does not move, so sphere-only kernels test both kinds with one 32-B branch-free test
-  // msphere: q0 = (c0x, c0y, c0z, r*r), q1 = (c1-c0 xyz, key bits), q2 = (t0, t1, r, -), aux = 1 if
+  // msphere: q0 = (c0x, c0y, c0z, r*r), q1 = (c1-c0 xyz, key bits), q2 = (t0, t1, r, RN(1/r)), aux = 1 if
   //          the shutter is [+0, 1] (center_at then needs no division and no q2)
   // rect   : q0 = (a0, a1, b0, b1), q1.x = k
   // tri    : q0 = (ax, ay, az, abx), q1 = (aby, abz, acx, acy), q2 = (acz, nx, ny, nz)
@@ -167,6 +167,7 @@ struct DevScene {
   uint32_t msphere_unit;  // every moving sphere's shutter is [+0, 1]: center_at needs no q2 / division
   uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
   float uni_off[3];
+  uint32_t rect_k_small;  // every rect's plane offset |k| < 2^62 (the rect test's reciprocal division guard)
 };
 
 struct DevCamera {

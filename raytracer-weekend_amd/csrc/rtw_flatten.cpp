@@ -140,6 +140,7 @@ struct Builder {
     memset(&p, 0, sizeof p);
     p.type_inst = PT_RECT_XY + axis;
     p.q0[0] = a0; p.q0[1] = a1; p.q0[2] = b0; p.q0[3] = b1; p.q1[0] = k;
+    if (!(fabsf(k) < 0x1p62f)) f.rect_k_small = 0;  // the kernel's reciprocal rect test then divides
     p.mat = mat;
     Box b;
     float lo[3], hi[3];
@@ -179,6 +180,10 @@ struct Builder {
         p.q2[0] = 0.0f;
         p.q2[1] = 1.0f;
         p.q2[2] = n.f[3];
+        {
+          const volatile float r = n.f[3];
+          p.q2[3] = 1.0f / r;  // RN(1 / r): the outward normal (p - c) / r by Markstein's correction (kernel)
+        }
         p.mat = n.mat;
         float r = fabsf(n.f[3]);  // |r|: spherical.rs:98-103 inverts the box for r < 0
         Box b;
@@ -201,6 +206,10 @@ struct Builder {
         p.q2[0] = n.f[3];
         p.q2[1] = n.f[7];
         p.q2[2] = n.f[8];  // r; q1[3] gets the key bits once keys are assigned
+        {
+          const volatile float r = n.f[8];
+          p.q2[3] = 1.0f / r;  // RN(1 / r) for the outward normal
+        }
         uint32_t t0_bits;
         memcpy(&t0_bits, &n.f[3], 4);
         p.aux = (t0_bits == 0u && n.f[7] == 1.0f) ? 1u : 0u;

@@ -82,7 +82,17 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
   if (__builtin_expect(!(x >= 0x1p-96f && x < INFINITY), 0)) r = sqrtf(x);
   return r;
 }
-__device__ __forceinline__ V3 unit(V3 a) { return divs(a, sqrtf(len2(a))); }       // vec3.rs:85-87
+#ifndef RTW_FAST_RCP
+#define RTW_FAST_RCP 1  // IEEE divisions by Markstein's correction from rcp_rn (below): unit(), normals, tris
+#endif
+#ifndef RTW_START_LDS
+#define RTW_START_LDS 1  // start_path's kernel-uniform operands from an LDS copy (StartArgs)
+#endif
+#ifndef RTW_RECT_RCP
+// list-mode rect tests from per-chain reciprocals (cand_rect_rcp): exact, but measured slower on cornell-800
+// (34.6k vs 35.5k Mrays/s with START_LDS; profiles/r03/experiments): off
+#define RTW_RECT_RCP 0
+#endif
 __device__ __forceinline__ bool near_zero(V3 a) {                                   // vec3.rs:133-138
   return fabsf(a.x) < 1e-8f && fabsf(a.y) < 1e-8f && fabsf(a.z) < 1e-8f;
 }
@@ -298,6 +308,50 @@ __device__ __forceinline__ float div_by_recip(float x, float b, float y) {
   const float r = __builtin_fmaf(-q0, b, x);
   return __builtin_fmaf(r, y, q0);
 }
+// RN(1 / b) in three VALU ops: the hardware reciprocal (v_rcp_f32, within 1 ulp) refined by one Newton
+// step with an exact residual, e = 1 - b y0 (fma), y1 = RN(y0 + e y0).  Equal to the IEEE quotient 1.0f / b
+// for every b with |b| in [2^-126, 2^126] (normal b whose reciprocal is normal): checked on the device over
+// all 2^32 bit patterns (rtw_diag_sweep 0, tests/test_gpu_parity.py), which is the proof, since v_rcp_f32
+// is a fixed function of its input.  Callers guard the range (rcp_rn_ok) and divide otherwise.
+__device__ __forceinline__ float rcp_rn_fast(float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, y0, 1.0f);
+  return __builtin_fmaf(e, y0, y0);
+}
+__device__ __forceinline__ bool rcp_rn_ok(float b) {
+  const float ab = fabsf(b);
+  return ab >= 0x1p-126f && ab <= 0x1p126f;
+}
+__device__ __forceinline__ float rcp_rn(float b) {  // = 1.0f / b for every b
+  float y = rcp_rn_fast(b);
+  if (__builtin_expect(!rcp_rn_ok(b), 0)) y = 1.0f / b;
+  return y;
+}
+// RN(x / b) from y = RN(1 / b) with the range guard of the sphere roots: Markstein's correction is the IEEE
+// quotient wherever b is in [2^-60, 2^60] and |x| < 2^64 and the quotient is normal, and below 2^-126 both
+// are tiny (< TMIN); other lanes divide.
+__device__ __forceinline__ bool recip_div_ok(float b) {
+  const float ab = fabsf(b);
+  return ab >= 0x1p-60f && ab <= 0x1p60f;
+}
+__device__ __forceinline__ float div_rcp(float x, float b, float y, bool b_ok) {
+  float t = div_by_recip(x, b, y);
+  if (__builtin_expect(!(b_ok && fabsf(x) < 0x1p64f), 0)) t = x / b;
+  return t;
+}
+// vec3.rs:85-87 unit_vector: a / |a|.  |a| = sqrt_rn (IEEE sqrt); the three divisions share the divisor, so
+// one rcp_rn and three corrections; |a.k| <= |a| needs no numerator guard.
+__device__ __forceinline__ V3 unit(V3 a) {
+#if RTW_FAST_RCP
+  const float s = sqrt_rn(len2(a));
+  const float y = rcp_rn_fast(s);
+  V3 r = mk(div_by_recip(a.x, s, y), div_by_recip(a.y, s, y), div_by_recip(a.z, s, y));
+  if (__builtin_expect(!recip_div_ok(s), 0)) r = divs(a, s);
+  return r;
+#else
+  return divs(a, sqrtf(len2(a)));
+#endif
+}
 
 // ---- candidate t of one primitive (independent of t_max; -1 = miss)
 // rad2 = radius * radius (precomputed for moving spheres; the same f32 product)
@@ -321,7 +375,11 @@ struct SphRcp { float a, ya; bool ok; };
 __device__ __forceinline__ SphRcp sph_rcp(const Ray& r) {
   SphRcp q;
   q.a = len2(r.d);
+#if RTW_FAST_RCP
+  q.ya = rcp_rn_fast(q.a);  // = 1.0f / a inside the guarded range below (outside it sph_div divides)
+#else
   q.ya = 1.0f / q.a;
+#endif
   q.ok = q.a >= 0x1p-60f && q.a <= 0x1p60f;
   return q;
 }
@@ -366,12 +424,51 @@ __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float 
   if (x < q0[0] || x > q0[1] || y < q0[2] || y > q0[3]) return -1.0f;
   return t;
 }
+// The rect test with the divisor's reciprocal computed once per wrapper chain (RectRcp: the object-space
+// direction's three components) instead of one IEEE division per rect: t = (k - o_k) / d_k by Markstein's
+// correction (3 VALU), the IEEE quotient wherever d_k is in [2^-60, 2^60] and |k - o_k| < 2^64.  The guard
+// is settled per chain too: |o_k| < 2^62 here and every rect's |k| < 2^62 (DevScene::rect_k_small, checked
+// by the flattener) bound the numerator.  A failed guard is stored as y = NaN (no lane masks to keep live:
+// the list-mode kernel is short of SGPRs), which makes the corrected quotient NaN, and those lanes divide.
+struct RectRcp {
+  float y[3];  // RN(1 / d.x), RN(1 / d.y), RN(1 / d.z), or NaN where the guard fails
+};
+__device__ __forceinline__ RectRcp rect_rcp(const Ray& r, uint32_t k_small) {
+  const float d[3] = {r.d.x, r.d.y, r.d.z}, o[3] = {r.o.x, r.o.y, r.o.z};
+  RectRcp q;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const bool ok = k_small && recip_div_ok(d[a]) && fabsf(o[a]) < 0x1p62f;
+    q.y[a] = ok ? rcp_rn_fast(d[a]) : __builtin_nanf("");
+  }
+  return q;
+}
+template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
+__device__ __forceinline__ float cand_rect_rcp(const Ray& r, const float* q0, float k, const RectRcp& rr) {
+  const float o_k = AXIS == 0 ? r.o.z : (AXIS == 1 ? r.o.y : r.o.x);
+  const float d_k = AXIS == 0 ? r.d.z : (AXIS == 1 ? r.d.y : r.d.x);
+  constexpr int KA = AXIS == 0 ? 2 : (AXIS == 1 ? 1 : 0);
+  const float o_a = AXIS == 2 ? r.o.y : r.o.x, d_a = AXIS == 2 ? r.d.y : r.d.x;
+  const float o_b = AXIS == 0 ? r.o.y : r.o.z, d_b = AXIS == 0 ? r.d.y : r.d.z;
+  const float n = k - o_k;
+  float t = div_by_recip(n, d_k, rr.y[KA]);  // finite wherever the guard held (n and y finite)
+  if (__builtin_expect(t != t, 0)) t = n / d_k;
+  if (t < TMIN) return -1.0f;
+  float x = o_a + t * d_a;
+  float y = o_b + t * d_b;
+  if (x < q0[0] || x > q0[1] || y < q0[2] || y > q0[3]) return -1.0f;
+  return t;
+}
 struct TriUV { float t, u, v; };
 __device__ __forceinline__ TriUV tri_solve(const Ray& r, const float* q) {  // triangular.rs:98-118
   V3 a = mk(q[0], q[1], q[2]), ab = mk(q[3], q[4], q[5]), ac = mk(q[6], q[7], q[8]);
   V3 n = mk(q[9], q[10], q[11]);
   float det = -dot(r.d, n);
+#if RTW_FAST_RCP
+  float inv = rcp_rn(det);  // triangular.rs:105 `1.0 / determinant`, the IEEE reciprocal
+#else
   float inv = 1.0f / det;
+#endif
   V3 ao = sub(r.o, a);
   V3 aoxd = cross(ao, r.d);
   TriUV o;
@@ -475,7 +572,8 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
 template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
-                                          uint32_t* cnt, uint64_t seg, const SphRcp* rq = nullptr) {
+                                          uint32_t* cnt, uint64_t seg, const SphRcp* rq = nullptr,
+                                          const RectRcp* rr = nullptr) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   // sphere-only worlds: a static sphere is tested as a moving one with c1 - c0 = 0 (c0 + time * 0 is
   // c0 up to the sign of a zero coordinate, which changes neither the decision nor t: the zero only
@@ -526,9 +624,15 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     t = cand_medium<FEAT>(S, lr, P, meta.y, meta.w, seg);
   } else if (FEAT & F_RECT) {
     const float k = q1v.x;
-    if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
-    else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
-    else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
+    if (rr) {  // LOCAL: rr holds the reciprocals of this very ray's direction
+      if (type == PT_RECT_XY) t = cand_rect_rcp<0>(lr, q0, k, *rr);
+      else if (type == PT_RECT_XZ) t = cand_rect_rcp<1>(lr, q0, k, *rr);
+      else if (type == PT_RECT_YZ) t = cand_rect_rcp<2>(lr, q0, k, *rr);
+    } else {
+      if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
+      else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
+      else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
+    }
   }
   if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }  // media: total only
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
@@ -571,14 +675,19 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
     uint32_t cur = 0;
     Ray lr = r;
+    // rect worlds: the reciprocals of the chain's direction once per chain, not a division per rect
+    constexpr bool RR = (FEAT & F_RECT) && RTW_RECT_RCP;
+    RectRcp rr;
+    if constexpr (RR) rr = rect_rcp(lr, S.rect_k_small);
     for (uint32_t k = 0; k < S.n_always; ++k) {
       const uint32_t pi = uload(S.always + k);
       const uint32_t inst = uload(&S.prims[pi].type_inst) >> 8;
       if (inst != cur) {
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
         cur = inst;
+        if constexpr (RR) rr = rect_rcp(lr, S.rect_k_small);
       }
-      test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg);
+      test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg, nullptr, RR ? &rr : nullptr);
     }
   } else {
     constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
@@ -861,7 +970,14 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     const float4 q0 = PP[0], q1 = PP[1];
     V3 c = type == PT_SPHERE ? mk(q0.x, q0.y, q0.z) : center_at(q0, q1, PP, S.msphere_unit, lr.time);
     const float rad = P.q2[2];  // r (q0.w holds r * r)
+#if RTW_FAST_RCP
+    // spherical.rs:49 (p - c) / r by the corrections from RN(1 / r), computed once by the flattener (q2.w)
+    const V3 pc = sub(h.p, c);
+    const bool ok = recip_div_ok(rad);
+    outward = mk(div_rcp(pc.x, rad, P.q2[3], ok), div_rcp(pc.y, rad, P.q2[3], ok), div_rcp(pc.z, rad, P.q2[3], ok));
+#else
     outward = divs(sub(h.p, c), rad);
+#endif
     if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
@@ -1075,7 +1191,28 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ bool start_path(const RenderArgs& a, uint64_t pid, PathState& st) {
+// start_path's kernel-uniform operands (camera, frame and tile geometry, seeds): copied into LDS once per
+// workgroup and re-read at every regeneration, instead of living in SGPRs across the whole path loop,
+// where the list-mode and sphere kernels had to spill them into VGPR lanes (every reload a v_readlane).
+struct StartArgs {
+  DevCamera cam;
+  float fw1, fh1, rw1, rh1, time_span;
+  uint32_t w, h, spp, max_depth, tiles_x, slot_base, tile_first, tile_stride;
+  uint64_t spp_magic, tiles_x_magic, seed_hash;
+  const uint32_t* tile_ids;
+};
+__device__ __forceinline__ void fill_start_args(const RenderArgs& a, StartArgs& o) {
+  o.cam = a.cam;
+  o.fw1 = a.fw1; o.fh1 = a.fh1; o.rw1 = a.rw1; o.rh1 = a.rh1; o.time_span = a.time_span;
+  o.w = a.w; o.h = a.h; o.spp = a.spp; o.max_depth = a.max_depth; o.tiles_x = a.tiles_x;
+  o.slot_base = a.slot_base; o.tile_first = a.tile_first; o.tile_stride = a.tile_stride;
+  o.spp_magic = a.spp_magic; o.tiles_x_magic = a.tiles_x_magic; o.seed_hash = a.seed_hash;
+  o.tile_ids = a.tile_ids;
+}
+
+template <bool FROM_LDS>
+__device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, PathState& st) {
+  if constexpr (FROM_LDS) asm volatile("" ::: "memory");  // read the LDS copy here: no loop-invariant register copies
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
   const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
   const uint32_t gslot = a.slot_base + slot;
@@ -1113,8 +1250,20 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
     const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) nodes_lds[k] = g[k];
-    __syncthreads();
   }
+  // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
+  // reload a v_readlane: cornell-800 +6%, jumpy +0.8%); the mesh variants regenerate paths every ~2
+  // segments and lost 5-7% to the LDS reads' latency, so they keep the kernel arguments
+  constexpr bool SLDS = RTW_START_LDS && !(FEAT & F_TRI);
+  __shared__ StartArgs start_lds[SLDS ? 1 : 0 + 1];
+  StartArgs sa_reg;
+  if constexpr (SLDS) {
+    if (threadIdx.x == 0) fill_start_args(a, start_lds[0]);
+  } else {
+    fill_start_args(a, sa_reg);
+  }
+  const StartArgs& SA = SLDS ? start_lds[0] : sa_reg;
+  __syncthreads();
   uint16_t* stk16 = stk16_all + threadIdx.x;
   int32_t* stk = stk_all + threadIdx.x;
   int32_t* spill = a.spill + (size_t)blockIdx.x * BLK + threadIdx.x;  // unused unless spill_depth > 0
@@ -1175,7 +1324,7 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path(a, id, st)) has = true;
+        if ((rank < avail || id < ne) && start_path<SLDS>(SA, id, st)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1354,6 +1503,35 @@ __global__ void libm_kernel(int fn, uint32_t n, const float* a, const float* b, 
   out[g] = fn == 0 ? dev_log10f(x) : (fn == 1 ? dev_sinf(x) : (fn == 2 ? dev_acosf(x) : dev_atan2f(x, b[g])));
 }
 
+// Diagnostics (rtw_diag_sweep): every 32-bit pattern in [lo, hi] as a float b, compared bit for bit
+// (NaN == NaN) against the IEEE operation.  fn 0: rcp_rn_fast(b) vs 1.0f / b over the range rcp_rn_ok
+// accepts (others are skipped: counted in n[1]).  n[0] = mismatches; the first `cap` are recorded.
+__global__ void sweep_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long long* n, uint32_t* bad, uint32_t cap) {
+  const uint64_t span = (uint64_t)hi - lo + 1u;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long nbad = 0, nskip = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < span; k += stride) {
+    const uint32_t bits = lo + (uint32_t)k;
+    const float b = __uint_as_float(bits);
+    bool ok = true;
+    if (fn == 0) {
+      if (!rcp_rn_ok(b)) {
+        ++nskip;
+        continue;
+      }
+      const float f = rcp_rn_fast(b), r = 1.0f / b;
+      ok = __float_as_uint(f) == __float_as_uint(r) || (f != f && r != r);
+    }
+    if (!ok) {
+      const unsigned long long slot = atomicAdd(n + 2, 1ull);
+      if (slot < cap) bad[slot] = bits;
+      ++nbad;
+    }
+  }
+  if (nbad) atomicAdd(n, nbad);
+  if (nskip) atomicAdd(n + 1, nskip);
+}
+
 }  // namespace dev
 
 // ---------------------------------------------------------------- host side
@@ -1418,6 +1596,7 @@ int upload(Scene& s, int device) {
     c.scene.n_insts = (uint32_t)f.insts.size();
     c.scene.msphere_unit = f.msphere_unit;
     c.scene.uni_inst = f.uni_inst;
+    c.scene.rect_k_small = f.rect_k_small;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
     s.dev.push_back(c);
   }
@@ -2009,6 +2188,34 @@ int rtw_diag_libm(int fn, uint32_t n, const float* a, const float* b, float* out
   if (da) hipFree(da);
   if (db) hipFree(db);
   if (dout) hipFree(dout);
+  return rc;
+}
+
+int rtw_diag_sweep(int fn, uint32_t lo, uint32_t hi, uint64_t* counts, uint32_t* bad, uint32_t cap) {
+  if (fn != 0 || lo > hi || !counts || (cap && !bad)) return fail(RTW_EINVAL, "bad arguments");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
+  unsigned long long* dn = nullptr;
+  uint32_t* dbad = nullptr;
+  int rc = RTW_OK;
+  if (hipMalloc((void**)&dn, 3 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc((void**)&dbad, (cap ? cap : 1) * sizeof(uint32_t)) != hipSuccess) {
+    rc = fail(RTW_ENOMEM, "hipMalloc(sweep)");
+  } else if (hipMemset(dn, 0, 3 * sizeof(unsigned long long)) != hipSuccess) {
+    rc = fail(RTW_ENODEV, "hipMemset(sweep)");
+  } else {
+    hipLaunchKernelGGL(dev::sweep_kernel, dim3(16384), dim3(256), 0, nullptr, fn, lo, hi, dn, dbad, cap);
+    unsigned long long h[3];
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h, dn, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
+        (cap && hipMemcpy(bad, dbad, cap * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)) {
+      rc = fail(RTW_ENODEV, "sweep_kernel");
+    } else {
+      counts[0] = h[0];
+      counts[1] = h[1];
+    }
+  }
+  if (dn) hipFree(dn);
+  if (dbad) hipFree(dbad);
   return rc;
 }
 

@@ -84,11 +84,11 @@ def test_corrupt_bvh_fails_every_path(gpu, monkeypatch, knob):
     s, cam, bg = _sphere_cloud(rtw)
     s.commit(device=0)
     assert s.info(3) >= 2 and s.info(5) == 0
-    rt = rtw.Raytracer(s, cam, bg, 16, 16, 1, seed=1)
+    rt = rtw.Raytracer(s, cam, bg, 8, 8, 1, seed=1)  # one wave: each walk runs 2^20 node-loop iterations
     good, _ = rt.render()
     s.render_status(0)  # nothing tripped yet
     s.diag_corrupt_bvh(0)
-    out = torch.zeros((16, 16, 3), dtype=torch.float32, device="cuda:0")
+    out = torch.zeros((8, 8, 3), dtype=torch.float32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     rt.render_device(out.data_ptr(), 0, 0, 0, stream)  # enqueued: no error yet
     with pytest.raises(rtw.RtwError) as e:

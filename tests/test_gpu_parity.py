@@ -369,3 +369,49 @@ def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
     ref, rays = orc.OracleScene(text, []).render(orc.camera_from_fields(cam.as_dict()), bg, w, h, spp, seed=5)
     assert st["rays"] == rays
     assert np.array_equal(g.view(np.uint32), ref.view(np.uint32))
+
+
+def test_fast_reciprocal_equals_ieee_for_every_float(gpu):
+    """rcp_rn (v_rcp_f32 + one Newton step with an exact fma residual) is the IEEE f32 reciprocal
+    1.0f / b for every bit pattern it is used on (|b| in [2^-126, 2^126]): an exhaustive device sweep
+    of all 2^32 patterns, so the rect / unit-vector / normal divisions built on it (Markstein's
+    correction from RN(1 / b)) are the reference's IEEE divisions (rectangular.rs:33-41, vec3.rs:85-87,
+    spherical.rs:49)."""
+    rtw = gpu
+    bad, skipped, first = rtw.diag_sweep(0, 0, 0xFFFFFFFF)
+    assert bad == 0, [hex(int(x)) for x in first[:8]]
+    # the skipped patterns are exactly those outside [2^-126, 2^126] in magnitude (and NaNs / infs)
+    inside = 2 * ((0x7E800000 - 0x00800000) + 1)
+    assert skipped == (1 << 32) - inside
+
+
+@pytest.mark.parametrize("case", ["far_plane", "far_origin", "near"])
+def test_rect_reciprocal_guard_paths_bit_exact(gpu, orc, case):
+    """The list-mode rect test divides by Markstein's correction from per-chain reciprocals of the ray
+    direction (cand_rect_rcp), guarded per chain: a rect plane |k| >= 2^62 (DevScene::rect_k_small = 0)
+    or a ray origin |o_k| >= 2^62 sends every lane to the IEEE division.  All three cases, with
+    wrapper chains (a rotated, translated cuboid), must match the oracle bit for bit."""
+    rtw = gpu
+    s = rtw.Scene()
+    red = s.lambertian_solid((0.65, 0.05, 0.05))
+    white = s.lambertian_solid((0.73, 0.73, 0.73))
+    light = s.diffuse_light(s.solid_rgb(7.0, 7.0, 7.0))
+    big = 1e25
+    far = 1e19 if case == "far_plane" else 300.0  # 1e19 > 2^62
+    s.xz_rect(-big, big, -big, big, far, light)                  # sky plane (y = k)
+    s.xz_rect(-big, big, -big, big, 0.0, white)                  # floor
+    s.yz_rect(0.0, 200.0, -200.0, 200.0, -150.0, red)            # a wall
+    with s.translate((40.0, 0.0, 20.0)), s.rotate_y(-18.0):
+        s.cuboid((0.0, 0.0, 0.0), (60.0, 120.0, 60.0), white)
+    text = s.dump()
+    s.commit()
+    if case == "far_origin":  # camera rays start at |o.z| >= 2^62: those chains' z guard fails, those lanes divide
+        cam = rtw.Camera.new((50.0, 80.0, 1e19), (50.0, 40.0, 0.0), (0, 1, 0), 50.0, 1.0, 0.0, 10.0)
+    else:
+        cam = rtw.Camera.new((50.0, 80.0, 400.0), (50.0, 40.0, 0.0), (0, 1, 0), 50.0, 1.0, 0.0, 10.0)
+    w, h, spp = 32, 32, 4
+    g, st = rtw.Raytracer(s, cam, (0.1, 0.1, 0.1), w, h, spp, seed=3).render()
+    r, rays = orc.OracleScene(text).render(orc.camera_from_fields(cam.as_dict()), (0.1, 0.1, 0.1), w, h, spp, seed=3)
+    assert st["rays"] == rays
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+    assert np.isfinite(g).all() and g.max() > 0
