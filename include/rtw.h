@@ -325,6 +325,9 @@ int64_t rtw_scene_info(const rtw_scene* s, int what);
  * numbered; csrc/rtw_device.hpp), valid once rtw_scene_commit has flattened the scene (also when its
  * upload failed for lack of a device).  *nodes points into the scene (read-only, lives as long as it). */
 int rtw_scene_nodes(const rtw_scene* s, const void** nodes, uint32_t* n_nodes);
+/* The same tree in half precision (DevNode4h, 112 B each: f16 plane offsets from an f16 origin, rounded
+ * outward; built when the 16-bit child codes fit, else *n_nodes = 0), as the kernels read it. */
+int rtw_scene_nodes_half(const rtw_scene* s, const void** nodes, uint32_t* n_nodes);
 
 #ifdef __cplusplus
 }

@@ -148,6 +148,7 @@ _SIGS = {
     "rtw_scene_dump": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rtw_scene_image": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(_U8), _U32, _U32]),
     "rtw_scene_nodes": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), _U32]),
+    "rtw_scene_nodes_half": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), _U32]),
     "rtw_scene_info": (C.c_int64, [C.c_void_p, C.c_int]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -424,6 +425,21 @@ class Scene:
         if not n.value:
             return np.zeros(0, dt)
         buf = (C.c_uint8 * (128 * n.value)).from_address(p.value)
+        return np.frombuffer(bytes(buf), dtype=dt).copy()
+
+
+    def nodes_half(self) -> np.ndarray:
+        """The half-precision BVH4 (DevNode4h, rtw_device.hpp) as a structured array (a copy; empty when
+        the 16-bit codes do not fit).  Planes are f16 offsets from `origin`: x[0] = lo x4, hi x4 and x[1] =
+        hi x4, lo x4 (likewise y, z)."""
+        p, n = C.c_void_p(), C.c_uint32()
+        _check(lib().rtw_scene_nodes_half(self._p, C.byref(p), C.byref(n)))
+        dt = np.dtype([("x", "<f2", (2, 8)), ("y", "<f2", (2, 8)), ("z", "<f2", (2, 8)), ("code", "<u2", 4),
+                       ("origin", "<f2", 3), ("pad", "<u2")])
+        assert dt.itemsize == 112
+        if not n.value:
+            return np.zeros(0, dt)
+        buf = (C.c_uint8 * (112 * n.value)).from_address(p.value)
         return np.frombuffer(bytes(buf), dtype=dt).copy()
 
 

@@ -553,6 +553,12 @@ int rtw_scene_nodes(const rtw_scene* s, const void** nodes, uint32_t* n_nodes) {
   *n_nodes = (uint32_t)s->s.flat.nodes4.size();
   return RTW_OK;
 }
+int rtw_scene_nodes_half(const rtw_scene* s, const void** nodes, uint32_t* n_nodes) {
+  if (!s || !nodes || !n_nodes) return fail(RTW_EINVAL, "NULL argument");
+  *nodes = s->s.flat.nodes4h.empty() ? nullptr : (const void*)s->s.flat.nodes4h.data();
+  *n_nodes = (uint32_t)s->s.flat.nodes4h.size();
+  return RTW_OK;
+}
 int64_t rtw_scene_info(const rtw_scene* s, int what) {
   if (!s) return -1;
   const Scene& sc = s->s;

@@ -66,6 +66,22 @@ struct alignas(16) DevNode4 {
 };
 static_assert(sizeof(DevNode4) == 128, "DevNode4 must be 128 B");
 
+// The same node in half precision (112 B, built when Flat::codes16): every plane is an f16 OFFSET from the
+// node's f16 origin (<= every child's lo), rounded outward (lo down, hi up: the box only grows, culling
+// stays conservative), so the precision follows the node's size, not its distance from the world origin.
+// Per axis the four children's planes are stored in both orders, [lo x4 | hi x4] and [hi x4 | lo x4], so a
+// lane loads its (near, far) planes with ONE 16-B load picked by its direction sign: a visit is 4 loads and
+// 64 B (3 plane loads + codes / origin) instead of 7 loads and 112 B.  The kernel evaluates
+// t = off * inv + (origin * inv - o * inv) with v_fma_mix_f32 (f16 operands, f32 arithmetic): no conversions.
+// Empty slots: lo = +inf, hi = -inf, as in DevNode4.
+struct alignas(16) DevNode4h {
+  uint16_t x[2][8], y[2][8], z[2][8];  // [0] = lo0..3, hi0..3; [1] = hi0..3, lo0..3 (f16 offsets)
+  uint16_t code[4];                    // DevNode4::code (16-bit child codes)
+  uint16_t origin[3];                  // f16, normal or zero
+  uint16_t pad;
+};
+static_assert(sizeof(DevNode4h) == 112, "DevNode4h must be 112 B");
+
 struct alignas(16) DevTriShade {
   float n[9];   // vertex normals after defaults (triangular.rs:55)
   float uv[6];  // vertex uvs after defaults (triangular.rs:57-66)
@@ -154,6 +170,7 @@ constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F
 
 struct DevScene {
   const DevNode4* nodes;
+  const DevNode4h* hnodes;  // the half-precision copy (nullptr unless Flat::codes16)
   const DevPrim* prims;
   const uint32_t* always;
   const DevTriShade* tshade;

@@ -502,6 +502,61 @@ struct Collapse {
   }
 };
 
+// ---- f16 with directed rounding (DevNode4h): binary search over the ordered f16 values
+double h2d(uint16_t h) {
+  const int e = (h >> 10) & 31, m = h & 1023;
+  const double v = e == 0 ? ldexp((double)m, -24) : (e == 31 ? (m ? NAN : INFINITY) : ldexp(1024.0 + m, e - 25));
+  return (h & 0x8000) ? -v : v;
+}
+uint16_t h_of_key(int32_t k) { return k >= 0 ? (uint16_t)k : (uint16_t)(0x8000 | -k); }
+// the largest f16 <= x (down) or the smallest f16 >= x (up); -inf / +inf beyond the range
+uint16_t h_round(double x, bool up) {
+  int32_t lo = -0x7C00, hi = 0x7C00;  // ordered keys of -inf .. +inf
+  if (up) {  // smallest key with h2d >= x
+    while (lo < hi) {
+      const int32_t mid = lo + (hi - lo) / 2;
+      if (h2d(h_of_key(mid)) >= x) hi = mid; else lo = mid + 1;
+    }
+  } else {  // largest key with h2d <= x
+    while (lo < hi) {
+      const int32_t mid = lo + (hi - lo + 1) / 2;
+      if (h2d(h_of_key(mid)) <= x) lo = mid; else hi = mid - 1;
+    }
+  }
+  return h_of_key(lo);
+}
+bool h_subnormal(uint16_t h) { return ((h >> 10) & 31) == 0 && (h & 1023) != 0; }
+// outward-rounded f16 offsets from a normal-or-zero f16 origin: no subnormal operand reaches the kernel
+void half_node(const DevNode4& n, DevNode4h& o) {
+  memset(&o, 0, sizeof o);
+  const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+  const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+  uint16_t* ax[3] = {&o.x[0][0], &o.y[0][0], &o.z[0][0]};
+  for (int a = 0; a < 3; ++a) {
+    double mn = INFINITY;
+    for (int k = 0; k < 4; ++k)
+      if (n.lo_x[k] <= n.hi_x[k]) mn = std::min(mn, (double)lo[a][k]);
+    uint16_t org = mn == INFINITY ? 0 : h_round(mn, false);
+    if (h_subnormal(org)) org = (org & 0x8000) ? 0x8400 : 0;  // -2^-14 or +0: still <= mn
+    o.origin[a] = org;
+    const double od = h2d(org);
+    for (int k = 0; k < 4; ++k) {
+      uint16_t l = 0x7C00, h = 0xFC00;  // empty slot: +inf, -inf
+      if (n.lo_x[k] <= n.hi_x[k]) {
+        l = h_round((double)lo[a][k] - od, false);  // >= 0 (od <= lo), rounded down
+        h = h_round((double)hi[a][k] - od, true);   // rounded up (+inf past 65504: conservative)
+        if (h_subnormal(l)) l = 0;
+        if (h_subnormal(h)) h = 0x0400;  // 2^-14
+      }
+      ax[a][k] = l;
+      ax[a][4 + k] = h;
+      ax[a][8 + k] = h;
+      ax[a][12 + k] = l;
+    }
+  }
+  for (int k = 0; k < 4; ++k) o.code[k] = (uint16_t)n.code[k];
+}
+
 bool texture_reads_uv(const Scene& s, uint32_t t, int guard = 0) {
   if (guard > 64) return false;
   const TexH& x = s.tex[t];
@@ -742,6 +797,10 @@ int flatten(Scene& s) {
           nd.code[k] = 0x8000u | ((first & 0x1FFFu) << 2) | ((cnt - 1u) & 3u);
         }
       }
+    if (f.codes16) {
+      f.nodes4h.resize(f.nodes4.size());
+      for (size_t q = 0; q < f.nodes4.size(); ++q) half_node(f.nodes4[q], f.nodes4h[q]);
+    }
   }
   // feature set (selects the specialised kernel)
   uint32_t F = 0;

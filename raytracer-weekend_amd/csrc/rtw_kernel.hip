@@ -723,11 +723,16 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // 44 of them the slab tests) and halves the stack's LDS.
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
-template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP>
+// HN: the walk reads the half-precision node table (DevNode4h: 4 loads / 64 B per visit instead of 7 / 112 B)
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2_t as_h2(uint32_t u) { return __builtin_bit_cast(half2_t, u); }
+
+template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP, bool HN = false>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
                           uint32_t* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
+  constexpr bool CODES = K16 || HN;  // leaves are 16-bit codes (the 32-bit walk keeps them sign-extended)
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
   if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
@@ -756,7 +761,8 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   // from the uniform table base: the loads take the SGPR-base + VGPR-offset form)
   const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
-  const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes) : reinterpret_cast<const char*>(S.nodes);
+  const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes)
+                                  : (HN ? reinterpret_cast<const char*>(S.hnodes) : reinterpret_cast<const char*>(S.nodes));
   // every wave must drain: a corrupt tree (a cycle) ends the walk instead of hanging the GPU, and
   // sets the device's host-mapped error word (RenderArgs::err), which the host turns into RTW_EINVAL
   // at the next render call, rtw_render_status, rtw_path_kernel_times or a stats read
@@ -818,37 +824,67 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       }
 #endif
       if (ts.node >= 0) {
-        const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
-        constexpr uint32_t CWO = K16 ? 112u : 96u;    // child codes (K16) or child words
-        float4 qnx, qfx, qny, qfy, qnz, qfz;
-        int4 cw;
-        {
-          qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
-          qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
-          qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
-          qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
-          qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
-          qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
-          cw = *reinterpret_cast<const int4*>(NB + (nb + CWO));
+        float NX[4], FX[4], NY[4], FY[4], NZ[4], FZ[4];
+        int32_t CW[4];
+        V3 bs;  // plane t = plane * inv + bs per axis
+        if constexpr (HN) {
+          // DevNode4h: per axis ONE 16-B load at offset 0 / 16 by direction sign = (near x4, far x4) as f16
+          // offsets; then codes + origin.  t = off * inv + (origin * inv - o * inv): every product and
+          // sum a v_fma_mix_f32 on the f16 halves.  The f16 boxes contain the f32 ones (outward rounding).
+          const uint32_t nb = (uint32_t)ts.node * 112u;  // sizeof(DevNode4h)
+          const uint4 px = *reinterpret_cast<const uint4*>(NB + (nb + nx));
+          const uint4 py = *reinterpret_cast<const uint4*>(NB + (nb + ny));
+          const uint4 pz = *reinterpret_cast<const uint4*>(NB + (nb + nz));
+          const uint4 cq = *reinterpret_cast<const uint4*>(NB + (nb + 96u));
+          const half2_t oxy = as_h2(cq.z), oz = as_h2(cq.w);
+          bs = mk(__builtin_fmaf((float)oxy.x, inv.x, -ood.x), __builtin_fmaf((float)oxy.y, inv.y, -ood.y),
+                  __builtin_fmaf((float)oz.x, inv.z, -ood.z));
+          const uint32_t P[3][4] = {{px.x, px.y, px.z, px.w}, {py.x, py.y, py.z, py.w}, {pz.x, pz.y, pz.z, pz.w}};
+          float* const NA[3] = {NX, NY, NZ};
+          float* const FA[3] = {FX, FY, FZ};
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const half2_t n01 = as_h2(P[a][0]), n23 = as_h2(P[a][1]), f01 = as_h2(P[a][2]), f23 = as_h2(P[a][3]);
+            NA[a][0] = (float)n01.x; NA[a][1] = (float)n01.y; NA[a][2] = (float)n23.x; NA[a][3] = (float)n23.y;
+            FA[a][0] = (float)f01.x; FA[a][1] = (float)f01.y; FA[a][2] = (float)f23.x; FA[a][3] = (float)f23.y;
+          }
+          if constexpr (K16) {  // the codes as they are
+            CW[0] = (int32_t)(cq.x & 0xFFFFu); CW[1] = (int32_t)(cq.x >> 16);
+            CW[2] = (int32_t)(cq.y & 0xFFFFu); CW[3] = (int32_t)(cq.y >> 16);
+          } else {  // sign-extended: internal >= 0, leaf < 0, as the 32-bit walk's child words
+            CW[0] = (int32_t)(int16_t)(cq.x & 0xFFFFu); CW[1] = (int32_t)cq.x >> 16;
+            CW[2] = (int32_t)(int16_t)(cq.y & 0xFFFFu); CW[3] = (int32_t)cq.y >> 16;
+          }
+        } else {
+          const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
+          constexpr uint32_t CWO = K16 ? 112u : 96u;    // child codes (K16) or child words
+          const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
+          const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
+          const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
+          const float4 qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
+          const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz));
+          const float4 qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
+          const int4 cw = *reinterpret_cast<const int4*>(NB + (nb + CWO));
+          bs = neg(ood);
+          NX[0] = qnx.x; NX[1] = qnx.y; NX[2] = qnx.z; NX[3] = qnx.w; FX[0] = qfx.x; FX[1] = qfx.y; FX[2] = qfx.z; FX[3] = qfx.w;
+          NY[0] = qny.x; NY[1] = qny.y; NY[2] = qny.z; NY[3] = qny.w; FY[0] = qfy.x; FY[1] = qfy.y; FY[2] = qfy.z; FY[3] = qfy.w;
+          NZ[0] = qnz.x; NZ[1] = qnz.y; NZ[2] = qnz.z; NZ[3] = qnz.w; FZ[0] = qfz.x; FZ[1] = qfz.y; FZ[2] = qfz.z; FZ[3] = qfz.w;
+          CW[0] = cw.x; CW[1] = cw.y; CW[2] = cw.z; CW[3] = cw.w;
         }
         if (COUNT) {
           cnt[0]++;
           simd_tick(cnt, 8, 9);
-          cnt[14] += (cw.x != 0) + (cw.y != 0) + (cw.z != 0) + (cw.w != 0);  // child word 0 = empty slot
+          cnt[14] += (CW[0] != 0) + (CW[1] != 0) + (CW[2] != 0) + (CW[3] != 0);  // child word 0 = empty slot
         }
         const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
         float tn[4];
         bool hit[4];
-        const int32_t CW[4] = {cw.x, cw.y, cw.z, cw.w};
-        const float NX[4] = {qnx.x, qnx.y, qnx.z, qnx.w}, FX[4] = {qfx.x, qfx.y, qfx.z, qfx.w};
-        const float NY[4] = {qny.x, qny.y, qny.z, qny.w}, FY[4] = {qfy.x, qfy.y, qfy.z, qfy.w};
-        const float NZ[4] = {qnz.x, qnz.y, qnz.z, qnz.w}, FZ[4] = {qfz.x, qfz.y, qfz.z, qfz.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // conservative slab test (culling only)
-          const float a = __builtin_fmaf(NX[k], inv.x, -ood.x), b = __builtin_fmaf(NY[k], inv.y, -ood.y);
-          const float c = __builtin_fmaf(NZ[k], inv.z, -ood.z);
-          const float d = __builtin_fmaf(FX[k], inv.x, -ood.x), e = __builtin_fmaf(FY[k], inv.y, -ood.y);
-          const float f = __builtin_fmaf(FZ[k], inv.z, -ood.z);
+          const float a = __builtin_fmaf(NX[k], inv.x, bs.x), b = __builtin_fmaf(NY[k], inv.y, bs.y);
+          const float c = __builtin_fmaf(NZ[k], inv.z, bs.z);
+          const float d = __builtin_fmaf(FX[k], inv.x, bs.x), e = __builtin_fmaf(FY[k], inv.y, bs.y);
+          const float f = __builtin_fmaf(FZ[k], inv.z, bs.z);
           tn[k] = fmaxf(fmaxf(fmaxf(a, b), c), 0.0f);
           hit[k] = tn[k] <= fminf(fminf(fminf(d, e), f), tmax_c);
         }
@@ -918,9 +954,9 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     if (g2 == GUARD) break;
     tick(0);
     if (ts.pend != 0) {  // phase 2
-      const uint32_t v = K16 ? (uint32_t)ts.pend : ~(uint32_t)ts.pend;
-      const int32_t first = K16 ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
-      const int32_t n = K16 ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
+      const uint32_t v = CODES ? (uint32_t)ts.pend & 0xFFFFu : ~(uint32_t)ts.pend;
+      const int32_t first = CODES ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
+      const int32_t n = CODES ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
       for (int32_t k = 0; k < n; ++k)
         test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
       ts.pend = 0;
@@ -1241,15 +1277,16 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
 
 // BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
-template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0>
+template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, bool HN = false>
 __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
   // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included)
   __shared__ int32_t stk_all[NCAP > 0 ? 1 : (STACK + 1) * BLK];
   __shared__ uint16_t stk16_all[NCAP > 0 ? STACK * BLK : 1];
-  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * 8 : 1];
+  constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
+  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
-    const float4* g = reinterpret_cast<const float4*>(a.scene.nodes);
-    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK) nodes_lds[k] = g[k];
+    const float4* g = HN ? reinterpret_cast<const float4*>(a.scene.hnodes) : reinterpret_cast<const float4*>(a.scene.nodes);
+    for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * NODE_Q; k += BLK) nodes_lds[k] = g[k];
   }
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
   // reload a v_readlane: cornell-800 +6%, jumpy +0.8%); the mesh variants regenerate paths every ~2
@@ -1351,7 +1388,7 @@ __global__ __launch_bounds__(BLK, OCC) void path_kernel(RenderArgs a) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
+      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP, HN>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
                                                       leaf_thr, st.rng, a.err, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
@@ -1562,7 +1599,7 @@ int upload(Scene& s, int device) {
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
-  size_t o_shade = put(blob, f.shade);
+  size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h);
   blob.resize((blob.size() + 255) & ~(size_t)255);
   int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
   int prev = 0;
@@ -1581,6 +1618,7 @@ int upload(Scene& s, int device) {
     *(volatile uint32_t*)c.err_host = 0u;
     uint8_t* base = (uint8_t*)c.block;
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
+    c.scene.hnodes = f.nodes4h.empty() ? nullptr : (const DevNode4h*)(base + o_hnodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
     c.scene.always = (const uint32_t*)(base + o_always);
     c.scene.tshade = (const DevTriShade*)(base + o_tsh);
@@ -1689,8 +1727,14 @@ constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
 // (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
 // from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
 template <bool C, uint32_t F>
-static Variant pick5(uint32_t need) {
+static Variant pick5(uint32_t need, bool half = false) {
   using namespace dev;
+  if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built
+    if (half && need <= (uint32_t)STACK_LDS5)
+      return {path_kernel<C, STACK_LDS5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_LDS5};
+    if (half && need <= (uint32_t)STACK_DEEP5)
+      return {path_kernel<C, STACK_DEEP5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_DEEP5};
+  }
   if (need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 5, F>, (uint32_t)STACK_LDS5};
   if constexpr (F == F_MESHES || F == F_ALL) {
     if (need <= (uint32_t)STACK_DEEP5) return {path_kernel<C, STACK_DEEP5, false, 5, F>, (uint32_t)STACK_DEEP5};
@@ -1704,6 +1748,14 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
+  // Half-precision nodes (DevNode4h, built when the 16-bit codes fit) trade vector-memory traffic (4 loads /
+  // 64 B per visit instead of 7 / 112 B) for VALU issue (v_fma_mix_f32 issues ~1.3x slower than v_fma_f32,
+  // scripts/ubench/mix_rate.hip; +5 VALU per visit).  Measured (profiles/r03/experiments, h1): monument-4k
+  // +3.3% (its 2,226-node tree), cow-1080p -6.5% (1,591 nodes), jumpy-1080p -4.9% (LDS nodes).  So by
+  // default only mesh trees of >= 2048 node4s use them; knob RTW_HALF_NODES 1 = wherever built, 0 = never.
+  const int half_knob = env_int("RTW_HALF_NODES", -1);
+  const bool half = codes16 && (half_knob > 0 || (half_knob < 0 && n_nodes >= 2048));
+  const bool half_lds = codes16 && half_knob > 0;
   if (list && !env_int("RTW_GENERIC", 0)) {
     // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
     // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
@@ -1725,9 +1777,13 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
     }
     case 6:
       if (sph && codes16 && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
-          env_int("RTW_LDS_NODES", 1))
+          env_int("RTW_LDS_NODES", 1)) {
+        if (half_lds)
+          return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP, true>, (uint32_t)LDSN_STACK,
+                  (uint32_t)LDSN_BLK, true};
         return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
                 (uint32_t)LDSN_BLK, true};
+      }
       if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
       [[fallthrough]];
     default:
@@ -1739,7 +1795,7 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
         // a partial LDS node cache (the top 128 / 376 / 760 node4s, the rest from global memory, sorted-push
         // walk) measured slower on cow / monument (profiles/r02/experiments, n7): the full-table kernels
         // are for trees that fit
-        return pick5<C, F_MESHES>(need);
+        return pick5<C, F_MESHES>(need, half);
       }
       return pick5<C, F_ALL>(need);
   }
@@ -2076,6 +2132,20 @@ int rtw_diag_corrupt_bvh(rtw_scene* s, int device) {
   DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemcpy(const_cast<DevNode4*>(c->scene.nodes), nd, sizeof nd, hipMemcpyHostToDevice), "hipMemcpy(nodes)");
+  if (c->scene.hnodes) {  // the half-precision table too: slot 0 = [-65504, +inf) on every axis, slots 1-3 empty
+    DevNode4h hn[2];
+    memset(hn, 0, sizeof hn);
+    for (DevNode4h& n : hn) {
+      for (uint16_t* ax : {&n.x[0][0], &n.y[0][0], &n.z[0][0]})
+        for (int k = 0; k < 4; ++k) {
+          const uint16_t lo = k ? 0x7C00 : 0x0000, hi = k ? 0xFC00 : 0x7C00;
+          ax[k] = lo; ax[4 + k] = hi; ax[8 + k] = hi; ax[12 + k] = lo;
+        }
+      n.origin[0] = n.origin[1] = n.origin[2] = 0xFBFF;  // -65504
+      n.code[0] = 1;
+    }
+    HIPCHK(hipMemcpy(const_cast<DevNode4h*>(c->scene.hnodes), hn, sizeof hn, hipMemcpyHostToDevice), "hipMemcpy(hnodes)");
+  }
   return RTW_OK;
 }
 

@@ -194,3 +194,35 @@ def test_camera_reciprocal_is_correctly_rounded(rtw):
     got = rtw.diag_recip(b)
     want = (np.float32(1.0) / b).astype(np.float32)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["jumpy-balls", "wavefront-cow-obj", "textured-monument", "book2-final-scene"])
+def test_half_nodes_contain_the_f32_boxes(rtw, name):
+    """DevNode4h (rtw_flatten.cpp half_node): every child's f16 box, origin + offsets, contains its padded
+    f32 box (lo rounded down, hi up), so the half-precision walk culls conservatively; empty slots stay
+    inverted; the two plane orders agree; the codes are DevNode4's; no f16 subnormal reaches the kernel
+    (the origin is normal or zero, offsets normal or zero)."""
+    s = rtw.Scene()
+    s.preset(name, 16 / 9, seed=3)
+    _commit_anywhere(rtw, s)
+    nd, nh = s.nodes(), s.nodes_half()
+    assert len(nh) == len(nd) > 0
+    for ax in ("x", "y", "z"):
+        lo32, hi32 = nd["lo_" + ax].astype(np.float64), nd["hi_" + ax].astype(np.float64)
+        h = nh[ax]
+        org = nh["origin"][:, "xyz".index(ax)].astype(np.float64)
+        lo16, hi16 = h[:, 0, :4].astype(np.float64), h[:, 0, 4:].astype(np.float64)
+        assert np.array_equal(h[:, 1, :4].view(np.uint16), h[:, 0, 4:].view(np.uint16))
+        assert np.array_equal(h[:, 1, 4:].view(np.uint16), h[:, 0, :4].view(np.uint16))
+        empty = nd["lo_x"] > nd["hi_x"]
+        assert np.all(np.isposinf(lo16[empty])) and np.all(np.isneginf(hi16[empty]))
+        full = ~empty
+        with np.errstate(invalid="ignore"):
+            assert np.all((org[:, None] + lo16 <= lo32)[full]), ax
+            assert np.all((org[:, None] + hi16 >= hi32)[full]), ax
+        bits = h.view(np.uint16)
+        sub = ((bits & 0x7C00) == 0) & ((bits & 0x3FF) != 0)
+        assert not sub.any()
+        ob = nh["origin"].view(np.uint16)
+        assert not (((ob & 0x7C00) == 0) & ((ob & 0x3FF) != 0)).any()
+    assert np.array_equal(nh["code"].astype(np.uint32), nd["code"])
