@@ -1,22 +1,31 @@
 // rtw_kernel.hip — gfx950 path-tracing megakernel and the device half of the C-ABI.
 //
 // Hot path restated (reference raytracer_weekend_lib/src/):
-//   Raytracer::render / sample_pixel (lib.rs:57-95)   -> one lane per pixel, samples in order
+//   Raytracer::render / sample_pixel (lib.rs:57-95)   -> one work unit per path (pixel, sample); the samples
+//                                                        of a pixel are summed in sample order afterwards
 //   sample_ray (lib.rs:97-117)                          -> iterative bounce loop, L = T * terminal
-//   [Box<dyn Hittable>]::hit (hittable/mod.rs:57-69)    -> BVH2 traversal, min t, ties -> max key
+//   [Box<dyn Hittable>]::hit (hittable/mod.rs:57-69)    -> 4-wide BVH walk (or the flat list), min t,
+//                                                        ties -> the larger DFS key
 //   Material::scatter / emitted (material.rs, light_source.rs), Texture::value (texture.rs,
 //   image_texture.rs), Camera::get_ray (camera.rs:66-74)
 //
 // Numerics: compiled with -ffp-contract=off and IEEE div/sqrt (hipcc's default
 // -fhip-fp32-correctly-rounded-divide-sqrt), so every primitive test, scatter and the
-// throughput product are bit-identical to the oracle's iterative integrator.  Only the
-// BVH culling uses FMA / rcp, and it is conservative (padded boxes + slack), so it
-// changes which nodes are visited, never the answer.
+// throughput product are bit-identical to the oracle's iterative integrator.  Divisions that
+// share a divisor use Markstein's correction from an exact reciprocal (rcp_rn, proven over every
+// float on the device).  Only the BVH culling uses FMA / rcp approximations, and it is
+// conservative (padded boxes + slack), so it changes which nodes are visited, never the answer.
 //
-// Wave structure: a workgroup is 4 waves; each wave owns one 8x8 pixel tile (coherent
-// camera rays).  A lane loops over its pixel's samples with path regeneration: every
-// loop iteration traces exactly one segment, and a lane whose path ended starts its
-// next sample in the same iteration, so lanes stay busy across paths of 1..50 bounces.
+// Kernel structure: path_kernel is PERSISTENT -- the grid is the resident capacity,
+// and each wave draws path ids from one global queue (2048 per atomic) into an LDS pool, hands them
+// to its idle lanes by ballot + mbcnt prefix (64 consecutive ids = one sample of one 8x8 tile), and
+// loops: regenerate -> trace_begin (the always-tested list) -> trace_run (resumable BVH4 walk with
+// postponed leaves; returns once quota16/16 of the lanes are done) -> shade.  A finished path writes
+// its radiance to an ordered sample buffer that reduce_kernel sums per pixel in sample order.
+// Variants (pick_kernel): feature-specialised instantiations; the LDS-node kernel (512-lane
+// workgroups, the whole node table in LDS, sorted-push walk over 16-bit child codes) for sphere
+// worlds that fit; the global-node kernels (256-lane workgroups, 32-bit LDS stack) for meshes, with
+// half-precision nodes (DevNode4h) for large trees; BVH-less list-mode kernels for <= 32 primitives.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
