@@ -185,6 +185,8 @@ struct DevScene {
   uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
   float uni_off[3];
   uint32_t rect_k_small;  // every rect's plane offset |k| < 2^62 (the rect test's reciprocal division guard)
+  uint32_t bvh_tri;       // every BVH leaf primitive is a triangle of instance tri_inst (the leaf fast path)
+  uint32_t tri_inst;
 };
 
 struct DevCamera {

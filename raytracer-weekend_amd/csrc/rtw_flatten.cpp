@@ -647,6 +647,32 @@ int flatten(Scene& s) {
     rest = B.leaves;
   }
 
+  // Triangle meshes: when the BVH part is all triangles of ONE wrapper chain but for a few other
+  // primitives (the cow's light rect), those few join the always-tested list, so every BVH leaf is a
+  // triangle of that chain (Flat::bvh_tri): the kernel's leaf test then skips the type dispatch and the
+  // per-test wrapper transform, and loads 3 x 16 B instead of 4 (the tie key only on a candidate hit).
+  // Which leaves are tested where never changes the answer (closest t, ties to the larger key).
+  {
+    size_t ntri = 0;
+    uint32_t inst = UINT32_MAX;
+    bool one_inst = true;
+    for (const Leaf& L : rest)
+      if ((L.p.type_inst & 0xffu) == PT_TRI) {
+        ++ntri;
+        const uint32_t i = L.p.type_inst >> 8;
+        if (inst == UINT32_MAX) inst = i;
+        one_inst = one_inst && i == inst;
+      }
+    const char* knob = getenv("RTW_TRI_LEAF");  // 0 = keep the mixed BVH and the generic leaf test
+    if ((!knob || atoi(knob)) && ntri > 16 && one_inst && rest.size() - ntri <= 4 &&
+        huge.size() + (rest.size() - ntri) <= 8) {
+      std::vector<Leaf> tris;
+      for (const Leaf& L : rest) ((L.p.type_inst & 0xffu) == PT_TRI ? tris : huge).push_back(L);
+      rest.swap(tris);
+      f.bvh_tri = 1;
+      f.tri_inst = inst;
+    }
+  }
   if (!rest.empty()) {
     uint32_t lg = 0;
     while ((1ull << lg) < rest.size()) ++lg;

@@ -652,6 +652,26 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   }
 }
 
+// A BVH leaf triangle when every leaf is a triangle of one wrapper chain (DevScene::bvh_tri): `lr` is
+// already the chain's object-space ray, no type dispatch; the 48 B of geometry in three loads, and the
+// tie key (DevPrim::key) only for a candidate at or below the best t (triangular.rs:97-138).
+template <bool COUNT>
+__device__ __forceinline__ void test_tri_leaf(const DevScene& S, uint32_t pi, const Ray& lr, Best& b, uint32_t* cnt) {
+  const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
+  const float4 q0v = P[0], q1v = P[1], q2v = P[2];
+  const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
+  const float t = cand_tri(lr, q);
+  if (COUNT) { cnt[1]++; cnt[2 + PT_TRI]++; simd_tick(cnt, 10, 11); }
+  if (t >= TMIN && t < INFINITY && t <= b.t) {  // hittable/mod.rs:61-65, the key read only here
+    const uint32_t key = reinterpret_cast<const uint4*>(P + 3)->y;
+    if (t < b.t || key > b.key) {
+      b.t = t;
+      b.key = key;
+      b.prim = (int32_t)pi;
+    }
+  }
+}
+
 // Conservative slab test on a padded box (culling only; never decides a hit).
 __device__ __forceinline__ bool slab_test(float lx, float ly, float lz, float hx, float hy, float hz,
                                           V3 inv, V3 ood, float tmax_c, float& tnear) {
@@ -745,6 +765,14 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
   if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
+  // triangle-only BVH (DevScene::bvh_tri): the leaves' common object-space ray, once per call
+  Ray tri_ray = r;
+  if constexpr ((FEAT & F_TRI) != 0) {
+    if (S.bvh_tri && (FEAT & F_INST) && S.tri_inst) {
+      if (S.tri_inst == S.uni_inst) tri_ray.o = sub(r.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
+      else tri_ray = to_local<true>(S.insts + S.tri_inst, r);
+    }
+  }
   // COUNT: tph[0] += wave-cycles in the node loop (phase 1), tph[1] += in the leaf tests (phase 2)
   uint64_t tm = COUNT ? __builtin_amdgcn_s_memtime() : 0;
   // Waves walking the tree issue before waves shading or regenerating (the path kernel drops the
@@ -966,8 +994,12 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
       const uint32_t v = CODES ? (uint32_t)ts.pend & 0xFFFFu : ~(uint32_t)ts.pend;
       const int32_t first = CODES ? (int32_t)((v >> 2) & 0x1FFFu) : (int32_t)(v >> 3);
       const int32_t n = CODES ? (int32_t)(v & 3u) + 1 : (int32_t)(v & 7u);
-      for (int32_t k = 0; k < n; ++k)
-        test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
+      if ((FEAT & F_TRI) && S.bvh_tri) {  // kernel-uniform: every leaf is a triangle of one wrapper chain
+        for (int32_t k = 0; k < n; ++k) test_tri_leaf<COUNT>(S, (uint32_t)(first + k), tri_ray, ts.b, cnt);
+      } else {
+        for (int32_t k = 0; k < n; ++k)
+          test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
+      }
       ts.pend = 0;
     }
     tick(1);
@@ -1644,6 +1676,8 @@ int upload(Scene& s, int device) {
     c.scene.msphere_unit = f.msphere_unit;
     c.scene.uni_inst = f.uni_inst;
     c.scene.rect_k_small = f.rect_k_small;
+    c.scene.bvh_tri = f.bvh_tri;  // knob RTW_TRI_LEAF (rtw_flatten.cpp)
+    c.scene.tri_inst = f.tri_inst;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
     s.dev.push_back(c);
   }
