@@ -1767,9 +1767,6 @@ struct Variant {
 // waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 224 node4s x 128 B + the pool
 // words = 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB): sphere worlds of up to ~850 spheres.
 constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
-#ifndef RTW_LDSN_OCC
-#define RTW_LDSN_OCC 6  // waves/SIMD the LDS-node kernel's registers are allocated for
-#endif
 // (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
 // from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
 template <bool C, uint32_t F>
@@ -1821,26 +1818,29 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       if (sph) return {sp ? path_kernel<C, STACK_LDS, true, 4, F_SPHERES> : path_kernel<C, STACK_LDS, false, 4, F_SPHERES>, st};
       return {sp ? path_kernel<C, STACK_LDS, true, 4, F_ALL> : path_kernel<C, STACK_LDS, false, 4, F_ALL>, st};
     }
-    case 6:
-      // 7 / 8 waves per SIMD: smaller LDS tables (448-lane workgroups x 4 per CU, 160 node4s, 18 stack rows;
-      // 512 x 4, 144 node4s, 16 rows) for the VGPR budget of 72 / 64 (knob RTW_LDSN_WAVES)
-      if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && env_int("RTW_LDSN_WAVES", 6) == 7 && need4 <= 18u &&
-          n_nodes <= 160u)
+    case 6: {
+      // 8 waves per SIMD when the tree fits a smaller table: 512-lane workgroups x 4 per CU, 144 node4s and 16
+      // stack rows in 36 KB of LDS, 64 VGPRs (the compiler spills 32 B per lane to scratch, outside the node
+      // loop).  The latency-bound kernel gains from the extra waves: jumpy-1080p 26.34k -> 27.02k Mrays/s
+      // (profiles/r03/experiments, w1); 7 waves (448-lane workgroups, 160 node4s, 18 rows, 72 VGPRs) measured
+      // slower (25.18k), as did both with half-precision nodes.  Knob RTW_LDSN_WAVES (6, 7, 8).
+      const int ldsn_waves = env_int("RTW_LDSN_WAVES", 8);
+      if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && ldsn_waves == 7 && need4 <= 18u && n_nodes <= 160u)
         return half_lds ? Variant{path_kernel<C, 18, false, 7, F_SPHERES, 448, 160, true>, 18u, 448u, true}
                         : Variant{path_kernel<C, 18, false, 7, F_SPHERES, 448, 160>, 18u, 448u, true};
-      if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && env_int("RTW_LDSN_WAVES", 6) == 8 && need4 <= 16u &&
-          n_nodes <= 144u)
+      if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && ldsn_waves == 8 && need4 <= 16u && n_nodes <= 144u)
         return half_lds ? Variant{path_kernel<C, 16, false, 8, F_SPHERES, 512, 144, true>, 16u, 512u, true}
                         : Variant{path_kernel<C, 16, false, 8, F_SPHERES, 512, 144>, 16u, 512u, true};
       if (sph && codes16 && need4 <= (uint32_t)LDSN_STACK && n_nodes <= (uint32_t)LDSN_CAP &&
           env_int("RTW_LDS_NODES", 1)) {
         if (half_lds)
-          return {path_kernel<C, LDSN_STACK, false, RTW_LDSN_OCC, F_SPHERES, LDSN_BLK, LDSN_CAP, true>, (uint32_t)LDSN_STACK,
+          return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP, true>, (uint32_t)LDSN_STACK,
                   (uint32_t)LDSN_BLK, true};
-        return {path_kernel<C, LDSN_STACK, false, RTW_LDSN_OCC, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
+        return {path_kernel<C, LDSN_STACK, false, 6, F_SPHERES, LDSN_BLK, LDSN_CAP>, (uint32_t)LDSN_STACK,
                 (uint32_t)LDSN_BLK, true};
       }
       if (sph && need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 6, F_SPHERES>, (uint32_t)STACK_LDS5};
+    }
       [[fallthrough]];
     default:
       if (env_int("RTW_GENERIC", 0)) return pick5<C, F_ALL>(need);  // parity of the generic kernel
