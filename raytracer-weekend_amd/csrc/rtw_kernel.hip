@@ -97,6 +97,9 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
 #ifndef RTW_START_LDS
 #define RTW_START_LDS 1  // start_path's kernel-uniform operands from an LDS copy (StartArgs)
 #endif
+#ifndef RTW_NT_SAMPLES
+#define RTW_NT_SAMPLES 1  // the sample buffer written with non-temporal stores
+#endif
 #ifndef RTW_RECT_RCP
 // list-mode rect tests from per-chain reciprocals (cand_rect_rcp): exact, but measured slower on cornell-800
 // (34.6k vs 35.5k Mrays/s with START_LDS; profiles/r03/experiments): off
@@ -1508,9 +1511,17 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     }
     if (done) {
       float* o = a.sbuf + (size_t)st.pid * 3u;  // one path's 12 B share a cache line
+#if RTW_NT_SAMPLES
+      // streaming stores: the 12.7 GB of samples per frame should not evict the scene tables and the
+      // register spill lines from L2 (they are read back once, by reduce_kernel)
+      __builtin_nontemporal_store(L.x, o);
+      __builtin_nontemporal_store(L.y, o + 1);
+      __builtin_nontemporal_store(L.z, o + 2);
+#else
       o[0] = L.x;
       o[1] = L.y;
       o[2] = L.z;
+#endif
       has = false;
     }
   }
@@ -1545,9 +1556,15 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   float x = 0.f, y = 0.f, z = 0.f;
   const float* q = a.sbuf + ((size_t)slot * a.spp * 64u + l) * 3u;
   for (uint32_t s = 0; s < a.spp; ++s, q += 64u * 3u) {
+#if RTW_NT_SAMPLES
+    x = x + __builtin_nontemporal_load(q);
+    y = y + __builtin_nontemporal_load(q + 1);
+    z = z + __builtin_nontemporal_load(q + 2);
+#else
     x = x + q[0];
     y = y + q[1];
     z = z + q[2];
+#endif
   }
   float* o = a.packed_out ? a.out + ((size_t)gslot * 64u + l) * 3u : a.out + ((size_t)row * a.w + i) * 3u;
   o[0] = x;
