@@ -495,8 +495,21 @@ __device__ __forceinline__ float cand_tri(const Ray& r, const float* q) {
   if (!(s.t >= 0.0f && s.u >= 0.0f && s.v >= 0.0f && (s.u + s.v) <= 1.0f)) return -1.0f;
   return s.t;
 }
+__device__ __forceinline__ float cand_tri_uv(const Ray& r, const float* q, float& u, float& v) {
+  TriUV s = tri_solve(r, q);
+  u = s.u;
+  v = s.v;
+  if (s.t < TMIN) return -1.0f;
+  if (!(s.t >= 0.0f && s.u >= 0.0f && s.v >= 0.0f && (s.u + s.v) <= 1.0f)) return -1.0f;
+  return s.t;
+}
 
-struct Best { float t; uint32_t key; int32_t prim; };
+struct Best {
+  float t;
+  uint32_t key;
+  int32_t prim;
+  float u, v;  // a triangle winner's barycentrics (tri_solve's, triangular.rs:109-112): the hit record reuses them
+};
 
 // ConstantMedium::hit (volumes.rs:37-78) in the order-independent form the oracle defines (K_MEDIUM):
 // boundary entry / exit by the reference's own hit routines with t in (-inf, inf) and
@@ -580,6 +593,20 @@ __device__ __forceinline__ void simd_tick(uint32_t* cnt, int wave_slot, int lane
   }
 }
 
+// The sphere-only kernels' branch-free 32-B test (q0 = (c0, r^2), q1 = (c1 - c0, key bits); see test_prim)
+__device__ __forceinline__ void test_sphere32(const DevScene& S, uint32_t pi, float4 q0v, float4 q1v, const Ray& wr,
+                                              Best& b, const SphRcp* rq) {
+  const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
+  const V3 c = center_at(q0v, q1v, P, S.msphere_unit, wr.time);
+  const float t = rq ? cand_sphere_rcp(wr, c, q0v.w, *rq) : cand_sphere(wr, c, q0v.w);
+  const uint32_t key = __float_as_uint(q1v.w);
+  if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
+    b.t = t;
+    b.key = key;
+    b.prim = (int32_t)pi;
+  }
+}
+
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
 template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
@@ -596,14 +623,7 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   if constexpr (SPH_ONLY && !COUNT) {
     const float4 q0v = UNI ? uload(P) : P[0];
     const float4 q1v = UNI ? uload(P + 1) : P[1];
-    const V3 c = center_at(q0v, q1v, P, S.msphere_unit, wr.time);
-    const float t = rq ? cand_sphere_rcp(wr, c, q0v.w, *rq) : cand_sphere(wr, c, q0v.w);
-    const uint32_t key = __float_as_uint(q1v.w);
-    if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && key > b.key))) {
-      b.t = t;
-      b.key = key;
-      b.prim = (int32_t)pi;
-    }
+    test_sphere32(S, pi, q0v, q1v, wr, b, rq);
     return;
   }
   // every 16-B part the scene's primitive kinds may need is loaded up front, in one round trip:
@@ -624,14 +644,14 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
       lr = to_local<UNI>(S.insts + inst, wr);
   }
   float q0[4] = {q0v.x, q0v.y, q0v.z, q0v.w};
-  float t = -1.0f;
+  float t = -1.0f, tu = 0.0f, tv = 0.0f;
   if ((FEAT & F_SPHERE) && type == PT_SPHERE) {
     t = cand_sphere(lr, mk(q0[0], q0[1], q0[2]), q0[3]);  // q0.w = r * r (flattener, the same f32 product)
   } else if ((FEAT & F_MSPHERE) && type == PT_MSPHERE) {
     t = cand_sphere(lr, center_at(q0v, q1v, P, S.msphere_unit, lr.time), q0v.w);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
-    t = cand_tri(lr, q);
+    t = cand_tri_uv(lr, q, tu, tv);
   } else if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {
     t = cand_medium<FEAT>(S, lr, P, meta.y, meta.w, seg);
   } else if (FEAT & F_RECT) {
@@ -652,6 +672,10 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     b.t = t;
     b.key = meta.y;
     b.prim = (int32_t)pi;
+    if (FEAT & F_TRI) {
+      b.u = tu;
+      b.v = tv;
+    }
   }
 }
 
@@ -663,7 +687,8 @@ __device__ __forceinline__ void test_tri_leaf(const DevScene& S, uint32_t pi, co
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   const float4 q0v = P[0], q1v = P[1], q2v = P[2];
   const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
-  const float t = cand_tri(lr, q);
+  float u, v;
+  const float t = cand_tri_uv(lr, q, u, v);
   if (COUNT) { cnt[1]++; cnt[2 + PT_TRI]++; simd_tick(cnt, 10, 11); }
   if (t >= TMIN && t < INFINITY && t <= b.t) {  // hittable/mod.rs:61-65, the key read only here
     const uint32_t key = reinterpret_cast<const uint4*>(P + 3)->y;
@@ -671,6 +696,8 @@ __device__ __forceinline__ void test_tri_leaf(const DevScene& S, uint32_t pi, co
       b.t = t;
       b.key = key;
       b.prim = (int32_t)pi;
+      b.u = u;
+      b.v = v;
     }
   }
 }
@@ -701,7 +728,7 @@ struct TraceState {
 template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
                                             uint64_t seg) {
-  ts.b = Best{INFINITY, 0u, -1};
+  ts.b = Best{INFINITY, 0u, -1, 0.0f, 0.0f};
   if (FEAT & F_INST) {
     // the always list is wave-uniform and in DFS order, so a wrapper chain's prims are adjacent
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
@@ -1031,8 +1058,22 @@ __device__ __forceinline__ void sphere_uv(V3 p, float& u, float& v) {  // spheri
 
 template <uint32_t FEAT>
 __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint32_t shade_kind) {
-  const DevPrim P = S.prims[b.prim];
-  const uint32_t type = P.type_inst & 0xffu, inst = P.type_inst >> 8;
+  // Triangle kernels: the meta word first, then only the geometry the winner's type needs (a triangle
+  // needs none: its barycentrics come from its test, Best::u / v; cow +4%).  Other kernels load the whole
+  // record in one round trip (a dependent geometry load cost jumpy 2.3%, profiles/r03/experiments b2).
+  const float4* PP = reinterpret_cast<const float4*>(S.prims + b.prim);
+  const uint4 meta = *reinterpret_cast<const uint4*>(PP + 3);
+  float4 g0, g1, g2;
+  if constexpr (!(FEAT & F_TRI)) {
+    g0 = PP[0];
+    g1 = PP[1];
+    g2 = PP[2];
+  }
+  auto geo = [&](int k) -> float4 {
+    if constexpr (!(FEAT & F_TRI)) return k == 0 ? g0 : (k == 1 ? g1 : g2);
+    else return PP[k];
+  };
+  const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
   const DevInst* I = S.insts + inst;
   const bool uni = (FEAT & F_INST) && inst && inst == S.uni_inst;  // one Translation, offset uniform
   Ray lr = wr;
@@ -1040,29 +1081,26 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   else if ((FEAT & F_INST) && inst) lr = to_local(I, wr);
   const float t = b.t;
   Rec h;
-  h.mat = P.mat;
+  h.mat = meta.z;
   h.u = 0.0f;
   h.v = 0.0f;
   V3 outward;
   h.p = add(lr.o, scale(lr.d, t));  // ray.rs:25-27
   if (((FEAT & F_SPHERE) && type == PT_SPHERE) || ((FEAT & F_MSPHERE) && type == PT_MSPHERE)) {
-    const float4* PP = reinterpret_cast<const float4*>(S.prims + b.prim);
-    const float4 q0 = PP[0], q1 = PP[1];
+    const float4 q0 = geo(0), q1 = geo(1), q2 = geo(2);
     V3 c = type == PT_SPHERE ? mk(q0.x, q0.y, q0.z) : center_at(q0, q1, PP, S.msphere_unit, lr.time);
-    const float rad = P.q2[2];  // r (q0.w holds r * r)
+    const float rad = q2.z;  // r (q0.w holds r * r)
 #if RTW_FAST_RCP
     // spherical.rs:49 (p - c) / r by the corrections from RN(1 / r), computed once by the flattener (q2.w)
     const V3 pc = sub(h.p, c);
     const bool ok = recip_div_ok(rad);
-    outward = mk(div_rcp(pc.x, rad, P.q2[3], ok), div_rcp(pc.y, rad, P.q2[3], ok), div_rcp(pc.z, rad, P.q2[3], ok));
+    outward = mk(div_rcp(pc.x, rad, q2.w, ok), div_rcp(pc.y, rad, q2.w, ok), div_rcp(pc.z, rad, q2.w, ok));
 #else
     outward = divs(sub(h.p, c), rad);
 #endif
     if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
-    const float q[12] = {P.q0[0], P.q0[1], P.q0[2], P.q0[3], P.q1[0], P.q1[1],
-                         P.q1[2], P.q1[3], P.q2[0], P.q2[1], P.q2[2], P.q2[3]};
-    TriUV s = tri_solve(lr, q);
+    const TriUV s{b.t, b.u, b.v};  // tri_solve's values from the winning test (the same ray and operands)
     const DevTriShade& sh = S.tshade[b.prim];  // indexed like prims[] (rtw_flatten.cpp)
     float w = 1.0f - s.u - s.v;  // triangular.rs:315-323
     outward = add(add(scale(ld3(sh.n), w), scale(ld3(sh.n + 3), s.u)), scale(ld3(sh.n + 6), s.v));
@@ -1074,8 +1112,9 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     const int axis = (int)type - PT_RECT_XY;
     const float x = axis == 2 ? h.p.y : h.p.x;
     const float y = axis == 0 ? h.p.y : h.p.z;
-    h.u = (x - P.q0[0]) / (P.q0[1] - P.q0[0]);
-    h.v = (y - P.q0[2]) / (P.q0[3] - P.q0[2]);
+    const float4 q0 = geo(0);
+    h.u = (x - q0.x) / (q0.y - q0.x);
+    h.v = (y - q0.z) / (q0.w - q0.z);
     outward = axis == 0 ? mk(0.f, 0.f, 1.f) : (axis == 1 ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f));
   }
   if ((FEAT & F_MEDIUM) && type == PT_MEDIUM) {
@@ -1453,7 +1492,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       // the prim's shading record is loaded as soon as the winner is known, beside its geometry
       // (one load instead of the prim -> material -> texture -> checker-child chain)
       const DevShade sh = S.shade[b.prim];
-      const Rec h = hit_record<FEAT>(S, st.ray, b, sh.kind);
+      // a light of one solid colour (light_source.rs:17-24 with SolidColor) needs no hit record: its
+      // emission is the colour and it never scatters (the cow's emitting mesh; mesh kernels only: the
+      // extra branch measured 0.7% slower on cornell-box)
+      const bool solid_light = (FEAT & F_LIGHT) && (FEAT & F_TRI) && (sh.kind & 0xfffu) == (MT_LIGHT | (SM_SOLID << 8));
+      Rec h;
+      if (!solid_light) h = hit_record<FEAT>(S, st.ray, b, sh.kind);
+      else h = Rec{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.0f, 0.0f, true, 0u};
       // One body for every material (material.rs:42-165, light_source.rs:17-24): a wave mixing
       // materials runs the rejection loop, unit() and the texture lookup once instead of once per
       // material branch.  Each material's draws and f32 operations are unchanged.
