@@ -100,6 +100,9 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
 #ifndef RTW_NT_SAMPLES
 #define RTW_NT_SAMPLES 1  // the sample buffer written with non-temporal stores
 #endif
+#ifndef RTW_RECT_SELECT
+#define RTW_RECT_SELECT 1  // rect tests and test_prim's accept as selects (kernels without triangles)
+#endif
 #ifndef RTW_RECT_RCP
 // list-mode rect tests from per-chain reciprocals (cand_rect_rcp): exact, but measured slower on cornell-800
 // (34.6k vs 35.5k Mrays/s with START_LDS; profiles/r03/experiments): off
@@ -141,13 +144,27 @@ __device__ __forceinline__ uint32_t rng_next(uint64_t& s) {
   s = ((uint64_t)s1 << 32) | s0;
   return result;
 }
+// (u >> 9) | 0x3F800000 (= 1.0f's bits: the float in [1, 2) with u's top 23 bits as mantissa) in one
+// v_alignbit_b32: the low word of the 64-bit (0x7F : u) >> 9.  Inline asm: the compiler turns the builtin
+// back into a shift and an or (two VALU ops per draw in the rejection loops).  AB = false keeps the shift and
+// the or: the asm statement changed the triangle kernels' register allocation (MI355X A/B,
+// profiles/r03/experiments r03t: jumpy +0.6%, cornell +1.0%, cow -2.4%, monument -1.2%), so only the
+// sphere and list-mode kernels use it (the same split as start_path's LDS operands, SLDS).
+template <bool AB>
+__device__ __forceinline__ uint32_t one_mant23(uint32_t u) {
+  if constexpr (!AB) return (u >> 9) | 0x3F800000u;
+  uint32_t r;
+  asm("v_alignbit_b32 %0, %1, %2, 9" : "=v"(r) : "s"(0x7Fu), "v"(u));
+  return r;
+}
 __device__ __forceinline__ float gen_f32(uint64_t& s) {  // rand Standard<f32>
   return (float)(rng_next(s) >> 8) * (1.0f / 16777216.0f);
 }
+template <bool AB>
 __device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi, float sc) {
   // UniformFloat::sample_single with sc = hi - lo precomputed (kernel-uniform: stays in an SGPR)
   for (;;) {
-    float v01 = __uint_as_float((rng_next(s) >> 9) | 0x3F800000u) - 1.0f;
+    float v01 = __uint_as_float(one_mant23<AB>(rng_next(s))) - 1.0f;
     float r = v01 * sc + lo;
     if (r < hi) return r;
     sc = __uint_as_float(__float_as_uint(sc) - 1u);
@@ -157,23 +174,29 @@ __device__ __forceinline__ float gen_range(uint64_t& s, float lo, float hi, floa
 // (v12 - 1) * 2 + -1 = 2 v12 - 3 = (m - 2^22) 2^-22 is exact in both forms and at most 1 - 2^-22 < 1,
 // so the retry never fires (checked for every m in tests/test_oracle_kat.py::test_pm1_never_retries)
 // and one exact fma gives the oracle's bits.
+template <bool AB>
 __device__ __forceinline__ float gen_pm1(uint64_t& s) {
-  const float v12 = __uint_as_float((rng_next(s) >> 9) | 0x3F800000u);
+  const float v12 = __uint_as_float(one_mant23<AB>(rng_next(s)));
   return __builtin_fmaf(v12, 2.0f, -3.0f);
 }
+template <bool AB>
 __device__ __forceinline__ V3 rand_in_unit_sphere(uint64_t& s) {  // vec3.rs:101-108
   for (;;) {
-    float x = gen_pm1(s);
-    float y = gen_pm1(s);
-    float z = gen_pm1(s);
+    float x = gen_pm1<AB>(s);
+    float y = gen_pm1<AB>(s);
+    float z = gen_pm1<AB>(s);
     V3 p = mk(x, y, z);
+#ifdef RTW_DIAG_ONE_TRIP  // timing diagnostic only (not the reference's distribution): no rejection tail
+    return p;
+#endif
     if (len2(p) < 1.0f) return p;
   }
 }
+template <bool AB>
 __device__ __forceinline__ V3 rand_in_unit_disk(uint64_t& s) {  // vec3.rs:124-131
   for (;;) {
-    float x = gen_pm1(s);
-    float y = gen_pm1(s);
+    float x = gen_pm1<AB>(s);
+    float y = gen_pm1<AB>(s);
     V3 p = mk(x, y, 0.0f);
     if (len2(p) < 1.0f) return p;
   }
@@ -423,13 +446,20 @@ __device__ __forceinline__ V3 center_at(float4 q0, float4 q1, const float4* P, u
   }
   return add(mk(q0.x, q0.y, q0.z), scale(mk(q1.x, q1.y, q1.z), frac));
 }
-template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
+template <int AXIS, bool SEL = false>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
 __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float k) {
   const float o_k = AXIS == 0 ? r.o.z : (AXIS == 1 ? r.o.y : r.o.x);
   const float d_k = AXIS == 0 ? r.d.z : (AXIS == 1 ? r.d.y : r.d.x);
   const float o_a = AXIS == 2 ? r.o.y : r.o.x, d_a = AXIS == 2 ? r.d.y : r.d.x;
   const float o_b = AXIS == 0 ? r.o.y : r.o.z, d_b = AXIS == 0 ? r.d.y : r.d.z;
   float t = (k - o_k) / d_k;
+  if constexpr (SEL) {
+    // the same decisions as selects (x, y have no side effects): no exec-mask branches in the list loop
+    const float x = o_a + t * d_a;
+    const float y = o_b + t * d_b;
+    const bool out = (t < TMIN) | (x < q0[0]) | (x > q0[1]) | (y < q0[2]) | (y > q0[3]);
+    return out ? -1.0f : t;
+  }
   if (t < TMIN) return -1.0f;
   float x = o_a + t * d_a;
   float y = o_b + t * d_b;
@@ -634,6 +664,9 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   const float4 q1v = NEED_Q1 ? (UNI ? uload(P + 1) : P[1]) : q0v;
   const float4 q2v = NEED_Q2 ? (UNI ? uload(P + 2) : P[2]) : q0v;
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
+  // rect tests and the accept as selects instead of exec-mask branches (RTW_RECT_SELECT) in the kernels
+  // without triangles: cornell-800 +6.7%; the triangle kernels lost 0.6-1.4% (profiles/r03/experiments, u1)
+  constexpr bool SEL = RTW_RECT_SELECT && !(FEAT & F_TRI);
   // object-space ray of the prim's wrapper chain; in BVH leaves recomputed per test (a few
   // flops) rather than cached, which keeps 8 VGPRs free for occupancy
   Ray lr = wr;
@@ -661,14 +694,19 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
       else if (type == PT_RECT_XZ) t = cand_rect_rcp<1>(lr, q0, k, *rr);
       else if (type == PT_RECT_YZ) t = cand_rect_rcp<2>(lr, q0, k, *rr);
     } else {
-      if (type == PT_RECT_XY) t = cand_rect<0>(lr, q0, k);
-      else if (type == PT_RECT_XZ) t = cand_rect<1>(lr, q0, k);
-      else if (type == PT_RECT_YZ) t = cand_rect<2>(lr, q0, k);
+      if (type == PT_RECT_XY) t = cand_rect<0, SEL>(lr, q0, k);
+      else if (type == PT_RECT_XZ) t = cand_rect<1, SEL>(lr, q0, k);
+      else if (type == PT_RECT_YZ) t = cand_rect<2, SEL>(lr, q0, k);
     }
   }
   if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }  // media: total only
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
-  if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && meta.y > b.key))) {
+  if constexpr (SEL) {
+    const bool acc = (t >= TMIN) & (t < INFINITY) & ((t < b.t) | ((t == b.t) & (meta.y > b.key)));
+    b.t = acc ? t : b.t;
+    b.key = acc ? meta.y : b.key;
+    b.prim = acc ? (int32_t)pi : b.prim;
+  } else if (t >= TMIN && t < INFINITY && (t < b.t || (t == b.t && meta.y > b.key))) {
     b.t = t;
     b.key = meta.y;
     b.prim = (int32_t)pi;
@@ -1345,12 +1383,12 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
   // lib.rs:84-86 + camera.rs:66-74
   const float u = div_by_recip((float)i + gen_f32(rng), a.fw1, a.rw1);
   const float v = div_by_recip((float)j + gen_f32(rng), a.fh1, a.rh1);
-  const V3 rd = scale(rand_in_unit_disk(rng), C.lens_radius);
+  const V3 rd = scale(rand_in_unit_disk<FROM_LDS>(rng), C.lens_radius);
   const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
   st.ray.o = add(ld3(C.origin), off);
   st.ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)), ld3(C.origin)),
                  off);
-  st.ray.time = gen_range(rng, C.time0, C.time1, a.time_span);
+  st.ray.time = gen_range<FROM_LDS>(rng, C.time0, C.time1, a.time_span);
   st.rng = rng;
   st.T = mk(1.f, 1.f, 1.f);
   st.depth = a.max_depth;
@@ -1509,7 +1547,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const bool iso = (FEAT & F_ISO) && mt == MT_ISOTROPIC;
       V3 rs = mk(0.f, 0.f, 0.f);
       phase(2);
-      if (lam || met || iso) rs = rand_in_unit_sphere(st.rng);  // vec3.rs:101-108
+      if (lam || met || iso) rs = rand_in_unit_sphere<SLDS>(st.rng);  // vec3.rs:101-108
       phase(3);
       const V3 ud = unit(lam ? rs : st.ray.d);                  // Lambertian: unit(rs); else unit(d_in)
       V3 att = mk(1.f, 1.f, 1.f);                                 // Dielectric: attenuation (1,1,1)
