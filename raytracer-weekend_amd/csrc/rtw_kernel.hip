@@ -794,7 +794,11 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
       test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg,
                                           (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
   }
-  ts.node = S.n_nodes ? 0 : -1;
+  // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR
+  // across the whole loop and spilled it
+  int32_t root = S.n_nodes ? 0 : -1;
+  asm volatile("" : "+v"(root));
+  ts.node = root;
   ts.pend = 0;
   ts.sp = 0;
   ts.on = true;
@@ -1367,8 +1371,10 @@ __device__ __forceinline__ void fill_start_args(const RenderArgs& a, StartArgs& 
   o.tile_ids = a.tile_ids;
 }
 
-template <bool FROM_LDS>
-__device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, PathState& st) {
+// LST_BLK > 0: also store T = 1, depth and the path id in the lane's LDS state rows (path_kernel LST), here
+// where the values are made (carried to the caller, they were spilled)
+template <bool FROM_LDS, int LST_BLK = 0, int LST_ROW = 0>
+__device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, PathState& st, uint16_t* lst = nullptr) {
   if constexpr (FROM_LDS) asm volatile("" ::: "memory");  // read the LDS copy here: no loop-invariant register copies
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
   const uint32_t slot = a.spp > 1u ? fastdiv(hi, a.spp_magic) : hi, s = hi - slot * a.spp;
@@ -1393,6 +1399,14 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
   st.T = mk(1.f, 1.f, 1.f);
   st.depth = a.max_depth;
   st.pid = (uint32_t)pid;
+  if constexpr (LST_BLK > 0) {
+    const uint32_t v[5] = {0x3F800000u, 0x3F800000u, 0x3F800000u, a.max_depth, (uint32_t)pid};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      lst[(LST_ROW + 2 * k) * LST_BLK] = (uint16_t)v[k];
+      lst[(LST_ROW + 2 * k + 1) * LST_BLK] = (uint16_t)(v[k] >> 16);
+    }
+  }
   return true;
 }
 
@@ -1402,7 +1416,9 @@ template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = B
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void path_kernel(RenderArgs a) {
   // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included)
   __shared__ int32_t stk_all[NCAP > 0 ? 1 : (STACK + 1) * BLK];
-  __shared__ uint16_t stk16_all[NCAP > 0 ? STACK * BLK : 1];
+  // LST: 10 more 16-bit rows after the stack hold the path state (below)
+  constexpr int LST_ROWS = (NCAP > 0 && BLK == 1024) ? 10 : 0;
+  __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : 1];
   constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
@@ -1426,6 +1442,21 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   int32_t* stk = stk_all + threadIdx.x;
   int32_t* spill = a.spill + (size_t)blockIdx.x * BLK + threadIdx.x;  // unused unless spill_depth > 0
   const uint32_t lane = threadIdx.x & 63u;
+  // LST (1024-lane LDS-node workgroups, 2 per CU: half the node-table copies of 512-lane ones): a path's
+  // throughput, remaining depth and id live in LDS, not VGPRs.  At 8 waves / SIMD (64 VGPRs) the compiler
+  // spilled exactly these to scratch (a scratch load / store per use in every shading pass: ~40% of the
+  // kernel's vector-memory instructions and ~23 GB of HBM write-back per jumpy-1080p frame)
+  // Each 32-bit value is two 16-bit rows of the lane's stack column (rows STACK.. STACK + 9: T.x, T.y, T.z,
+  // depth, id), addressed from the stack pointer with constant offsets: separate per-lane LDS pointers were
+  // loop-invariant VGPRs, which the compiler spilled in turn.
+  constexpr bool LST = LST_ROWS > 0;
+  auto lst_st = [&](int k, uint32_t v) {
+    stk16[(STACK + 2 * k) * BLK] = (uint16_t)v;
+    stk16[(STACK + 2 * k + 1) * BLK] = (uint16_t)(v >> 16);
+  };
+  auto lst_ld = [&](int k) -> uint32_t {
+    return (uint32_t)stk16[(STACK + 2 * k) * BLK] | ((uint32_t)stk16[(STACK + 2 * k + 1) * BLK] << 16);
+  };
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
   const uint64_t P = a.n_paths;
@@ -1482,7 +1513,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS>(SA, id, st)) has = true;
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, STACK>(SA, id, st, stk16)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1523,13 +1554,23 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     const Best b = ts.b;
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
+    const V3 T = LST ? mk(__uint_as_float(lst_ld(0)), __uint_as_float(lst_ld(1)), __uint_as_float(lst_ld(2))) : st.T;
     if (b.prim < 0) {  // lib.rs:102-105
-      L = mul(st.T, bg);
+      L = mul(T, bg);
       done = true;
     } else {
       // the prim's shading record is loaded as soon as the winner is known, beside its geometry
       // (one load instead of the prim -> material -> texture -> checker-child chain)
-      const DevShade sh = S.shade[b.prim];
+      // (LST: the second half, the checker's even colour, is read where it is used: held across the hit
+      // record it was spilled to scratch)
+      DevShade sh;
+      if constexpr (LST) {
+        const float4 q = *reinterpret_cast<const float4*>(S.shade + b.prim);
+        sh.kind = __float_as_uint(q.x); sh.param = q.y; sh.a[0] = q.z; sh.a[1] = q.w;
+        sh.a[2] = S.shade[b.prim].a[2];
+      } else {
+        sh = S.shade[b.prim];
+      }
       // a light of one solid colour (light_source.rs:17-24 with SolidColor) needs no hit record: its
       // emission is the colour and it never scatters (the cow's emitting mesh; mesh kernels only: the
       // extra branch measured 0.7% slower on cornell-box)
@@ -1556,11 +1597,12 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       } else if (light || lam || iso) {
         if (mode == SM_SOLID) att = ld3(sh.a);  // SolidColor::value
         else if ((FEAT & F_CHECKER) && mode == SM_CHECKER)
-          att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a) : ld3(sh.b);
+          att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a)
+                                                                                   : ld3(LST ? S.shade[b.prim].b : sh.b);
         else if (FEAT & F_TEXGEN) att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
       }
       if (light) {  // emit, no scatter
-        L = mul(st.T, att);
+        L = mul(T, att);
         done = true;
       } else {
         V3 dir = rs;  // Isotropic (material.rs:155-165): never absorbs
@@ -1586,14 +1628,29 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           if (cannot || reflectance(cos_t, r0) > gen_f32(st.rng)) dir = reflect(ud, h.n);
           else dir = refract(ud, h.n, ratio);
         }
-        st.T = mul(st.T, att);  // x * 1.0f == x: the Dielectric's T is unchanged
+        const V3 T2 = mul(T, att);  // x * 1.0f == x: the Dielectric's T is unchanged
+        if constexpr (LST) {
+          lst_st(0, __float_as_uint(T2.x));
+          lst_st(1, __float_as_uint(T2.y));
+          lst_st(2, __float_as_uint(T2.z));
+        } else {
+          st.T = T2;
+        }
         st.ray.o = h.p;
         st.ray.d = dir;
       }
-      if (!done && --st.depth == 0) done = true;  // lib.rs:98-100: depth 0 returns black
+      if (!done) {  // lib.rs:98-100: depth 0 returns black
+        if constexpr (LST) {
+          const uint32_t d = lst_ld(3) - 1u;
+          lst_st(3, d);
+          done = d == 0u;
+        } else {
+          done = --st.depth == 0u;
+        }
+      }
     }
     if (done) {
-      float* o = a.sbuf + (size_t)st.pid * 3u;  // one path's 12 B share a cache line
+      float* o = a.sbuf + (size_t)(LST ? lst_ld(4) : st.pid) * 3u;  // one path's 12 B share a cache line
 #if RTW_NT_SAMPLES
       // streaming stores: the 12.7 GB of samples per frame should not evict the scene tables and the
       // register spill lines from L2 (they are read back once, by reduce_kernel)
@@ -1928,6 +1985,12 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && ldsn_waves == 7 && need4 <= 18u && n_nodes <= 160u)
         return half_lds ? Variant{path_kernel<C, 18, false, 7, F_SPHERES, 448, 160, true>, 18u, 448u, true}
                         : Variant{path_kernel<C, 18, false, 7, F_SPHERES, 448, 160>, 18u, 448u, true};
+      // 1024-lane workgroups x 2 per CU (knob RTW_LDSN_BLK, 512 = the 4 x 512 form): one node table per 16
+      // waves, and the LDS this frees holds the paths' T / depth / id (path_kernel LST) that the 64-VGPR
+      // budget otherwise spills to scratch.  LDS per workgroup: 18 KB nodes + 32 KB stack + 20 KB state.
+      if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && ldsn_waves == 8 && need4 <= 16u && n_nodes <= 144u &&
+          !half_lds && env_int("RTW_LDSN_BLK", 1024) == 1024)
+        return Variant{path_kernel<C, 16, false, 8, F_SPHERES, 1024, 144>, 16u, 1024u, true};
       if (sph && codes16 && env_int("RTW_LDS_NODES", 1) && ldsn_waves == 8 && need4 <= 16u && n_nodes <= 144u)
         return half_lds ? Variant{path_kernel<C, 16, false, 8, F_SPHERES, 512, 144, true>, 16u, 512u, true}
                         : Variant{path_kernel<C, 16, false, 8, F_SPHERES, 512, 144>, 16u, 512u, true};

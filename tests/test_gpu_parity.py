@@ -115,7 +115,8 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
 @pytest.mark.parametrize("knob", ["RTW_REGEN_MIN=1", "RTW_REGEN_MIN=64", "RTW_QUOTA16=1", "RTW_QUOTA16=16",
                                   "RTW_LIST_MAX=0", "RTW_LIST_MAX=64", "RTW_LIST_OCC=6", "RTW_LEAF16=1",
                                   "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5", "RTW_HALF_NODES=1",
-                                  "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7"])
+                                  "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7",
+                                  "RTW_LDSN_BLK=512"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
@@ -351,11 +352,13 @@ def _sphere_world(rtw, seed, n=120):
     return s, cam, (0.7, 0.8, 1.0)
 
 
-@pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7", "RTW_HALF_NODES=1"])
+@pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7", "RTW_HALF_NODES=1",
+                                  "RTW_LDSN_BLK=512"])
 @pytest.mark.parametrize("seed,n", [(1, 120), (2, 120), (3, 700)])
 def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
     """Sphere worlds run the LDS-node kernel (node table in LDS, sorted-push walk over 16-bit codes)
-    when their tree fits -- the 8-wave variant for trees of <= 144 node4s (the 120-sphere worlds), the
+    when their tree fits -- the 8-wave variant for trees of <= 144 node4s (the 120-sphere worlds: 1024-lane
+    workgroups with the paths' T / depth / id in LDS, or the 512-lane form by knob), the
     6-wave one up to 224 (the 700-sphere world) -- else the global-node one: all bit-exact against the
     oracle, with equal ray counts, on worlds that mix every sphere kind and material the sphere kernels
     specialise for; likewise the 6 / 7-wave and half-precision-node variants by knob."""
