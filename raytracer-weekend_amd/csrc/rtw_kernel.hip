@@ -100,9 +100,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
 #ifndef RTW_NT_SAMPLES
 #define RTW_NT_SAMPLES 1  // the sample buffer written with non-temporal stores
 #endif
-#ifndef RTW_TRI_CROSS
-#define RTW_TRI_CROSS 0  // triangle-leaf test: normal recomputed from the edges (36 B loaded instead of 48)
-#endif
 #ifndef RTW_RECT_SELECT
 #define RTW_RECT_SELECT 1  // rect tests and test_prim's accept as selects (kernels without triangles)
 #endif
@@ -726,17 +723,8 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
 template <bool COUNT>
 __device__ __forceinline__ void test_tri_leaf(const DevScene& S, uint32_t pi, const Ray& lr, Best& b, uint32_t* cnt) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
-#if RTW_TRI_CROSS
-  // 36 B instead of 48: the plane normal (b - a) x (c - a) recomputed from the edges, the same f32 products
-  // and differences as the flattener's (vec3.rs cross), so the same bits
-  const float4 q0v = P[0], q1v = P[1];
-  const float acz = reinterpret_cast<const float*>(P + 2)[0];
-  const V3 nab = mk(q0v.w, q1v.x, q1v.y), nac = mk(q1v.z, q1v.w, acz), nn = cross(nab, nac);
-  const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, acz, nn.x, nn.y, nn.z};
-#else
   const float4 q0v = P[0], q1v = P[1], q2v = P[2];
   const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
-#endif
   float u, v;
   const float t = cand_tri_uv(lr, q, u, v);
   if (COUNT) { cnt[1]++; cnt[2 + PT_TRI]++; simd_tick(cnt, 10, 11); }
