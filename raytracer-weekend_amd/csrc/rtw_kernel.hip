@@ -100,9 +100,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
 #ifndef RTW_NT_SAMPLES
 #define RTW_NT_SAMPLES 1  // the sample buffer written with non-temporal stores
 #endif
-#ifndef RTW_RECT_MK
-#define RTW_RECT_MK 0  // select-form rect tests: t by Markstein's correction from a per-rect RN(1 / d)
-#endif
 #ifndef RTW_RECT_SELECT
 #define RTW_RECT_SELECT 1  // rect tests and test_prim's accept as selects (kernels without triangles)
 #endif
@@ -455,20 +452,7 @@ __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float 
   const float d_k = AXIS == 0 ? r.d.z : (AXIS == 1 ? r.d.y : r.d.x);
   const float o_a = AXIS == 2 ? r.o.y : r.o.x, d_a = AXIS == 2 ? r.d.y : r.d.x;
   const float o_b = AXIS == 0 ? r.o.y : r.o.z, d_b = AXIS == 0 ? r.d.y : r.d.z;
-#if RTW_RECT_MK
-  // SEL kernels: the quotient by Markstein's correction from this rect's own RN(1 / d_k) (no state carried
-  // across the list loop); the IEEE quotient wherever d_k is in [2^-60, 2^60] and |k - o_k| < 2^64, and
-  // other lanes divide (div_rcp)
-  float t;
-  if constexpr (SEL) {
-    const float n = k - o_k;
-    t = div_rcp(n, d_k, rcp_rn_fast(d_k), recip_div_ok(d_k));
-  } else {
-    t = (k - o_k) / d_k;
-  }
-#else
   float t = (k - o_k) / d_k;
-#endif
   if constexpr (SEL) {
     // the same decisions as selects (x, y have no side effects): no exec-mask branches in the list loop
     const float x = o_a + t * d_a;
