@@ -204,8 +204,7 @@ struct RenderArgs {
   uint32_t quota16;           // trace_run returns once quota16/16 of the wave's lanes are done
   uint32_t leaf16;            // postponed leaves are tested once leaf16/16 of the wave's lanes hold one and are stuck
   uint32_t regen_min;         // regenerate once this many lanes are idle (or every lane is)
-  uint32_t batch;             // path ids a wave takes from the global queue per atomic (the cap, when guided)
-  uint32_t guide_shift;       // > 0: guided batches of min(batch, remaining >> guide_shift), at least 64
+  uint32_t batch;             // path ids a wave takes from the global queue per atomic
   uint64_t spp_magic;         // UINT64_MAX / spp + 1 (dev::fastdiv; spp >= 2)
   float fw1, fh1;             // (float)(w - 1), (float)(h - 1) (lib.rs:84-85 divisors)
   float rw1, rh1;             // RN(1 / fw1), RN(1 / fh1): the camera divisions by Markstein's correction

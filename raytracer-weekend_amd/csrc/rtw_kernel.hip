@@ -1464,7 +1464,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
   // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
-  __shared__ uint64_t pool_lds[BLK / 64][4];
+  __shared__ uint64_t pool_lds[BLK / 64][3];
   uint64_t* const pool = pool_lds[threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
   bool exhausted = false;                // wave-uniform
@@ -1501,24 +1501,11 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       if (avail < n_need) {  // refill: one atomic per BATCH paths
         // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        // Guided batches (a.guide_shift > 0): a wave takes min(batch, remaining >> guide_shift) ids, at least
-        // 64, so the last ids of the frame go out in small batches and the waves finish together instead
-        // of the frame waiting on the waves that took the last full batches
-        if (lane == 0) {
-          uint64_t bs = a.batch;
-          if (a.guide_shift) {
-            const uint64_t q = __hip_atomic_load(a.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t g = (P > q ? P - q : 0) >> a.guide_shift;
-            bs = g < 64u ? 64u : (g < bs ? g : bs);
-          }
-          pool[2] = atomicAdd(a.queue, (unsigned long long)bs);
-          pool[3] = bs;
-        }
+        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)a.batch);
         const uint64_t b = rfl64(pool[2]);
         if (b < P) {
-          const uint64_t bs = rfl64(pool[3]);
           nb = b;
-          ne = b + bs < P ? b + bs : P;
+          ne = b + a.batch < P ? b + a.batch : P;
         } else {
           exhausted = true;
         }
@@ -2121,7 +2108,6 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   a.packed_out = (d_tiles || ts.packed) ? 1u : 0u;
   a.err = c.err_host;
   a.batch = (uint32_t)std::min(65536, std::max(64, env_int("RTW_BATCH", (int)dev::BATCH)));
-  a.guide_shift = 0;  // set below from the resident grid (RTW_GUIDE)
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
   if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
   // test postponed leaves once leaf16/16 of the wave's lanes hold one and cannot descend (trace_run);
@@ -2167,14 +2153,6 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
     a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
     const int grid = resident_grid(c, fn, var.block, count);
-    // guided batch sizes: remaining ids / 2^guide_shift with 2^guide_shift >= RTW_GUIDE x the resident waves
-    // (0 = fixed batches)
-    if (const int gk = env_int("RTW_GUIDE", 0); gk > 0) {
-      const uint64_t waves = (uint64_t)grid * (var.block / 64u) * (uint64_t)gk;
-      uint32_t sh = 0;
-      while ((1ull << sh) < waves) ++sh;
-      a.guide_shift = sh;
-    }
     // the LDS-node variants walk 16-bit codes within their own stack rows (pick_kernel checked
     // stack_need4 against them) and have no HBM spill path
     const uint32_t lds = var.stack;
