@@ -2145,9 +2145,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     // jumpy-balls (+0.5% over 3; profiles/r02/experiments, n5)
     if (var.k16 && sc.flat.features == (sc.flat.features & F_SPHERES))
       a.leaf16 = (uint32_t)std::min(16, std::max(1, env_int("RTW_LEAF16", 5)));
-    // the 1024-lane LDS-node kernel: 1024 ids per atomic (a shorter end-of-frame tail; jumpy-1080p +1.2% over
-    // 2048, profiles/r03/experiments k3); the other kernels keep 2048 (the meshes' short paths need it)
-    if (var.k16 && var.block == 1024u)
+    // the 1024-lane LDS-node kernel and the BVH-less list kernels: 1024 ids per atomic (a shorter end-of-frame
+    // tail; jumpy-1080p +1.2%, cornell-800 +0.5% over 2048, profiles/r03/experiments k3 / k4); the mesh
+    // kernels keep 2048 (neutral on cow; their short paths made small batches costly in round 2)
+    if ((var.k16 && var.block == 1024u) || sc.flat.nodes4.empty())
       a.batch = (uint32_t)std::min(65536, std::max(64, env_int("RTW_BATCH", 1024)));
     // Regenerate paths only once >= regen_min lanes of a wave are idle (or all are): start_path
     // runs at wave level, so batching it raises its SIMD utilisation.  Measured on MI355X
