@@ -3,7 +3,12 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config jumpy-1080p]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
-    python bench.py --multi-device N      # one process drives N GPUs through rtw_render_multi
+
+`--gpus N` always means N GPUs.  Under a launcher (WORLD_SIZE set) it must equal WORLD_SIZE: one
+process per GPU, one RCCL all-gather.  Without a launcher and N > 1, this one process drives the N GPUs
+through the C-ABI's rtw_render_multi (one RCCL send/recv gather to device 0); with fewer than N visible
+GPUs it exits non-zero before rendering anything.  `--multi-device N` is the same single-process path
+(also at N = 1).  The printed n_gpus is checked against N before the line is printed.
 
 A step = one full frame of the configured workload (default: BASELINE.json configs[1],
 RTOW final random-spheres "jumpy-balls", 1920x1080, 512 spp, 50 bounces) rendered by the
@@ -179,9 +184,31 @@ def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: in
     return out
 
 
+def resolve_gpus(args, world: int, visible: int) -> int:
+    """How many GPUs this process drives through rtw_render_multi (0 = the one-GPU / one-rank path).
+    Raises SystemExit (non-zero) instead of ever measuring fewer GPUs than --gpus asks for."""
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: at least 1")
+    if args.multi_device and args.gpus not in (None, args.multi_device):
+        raise SystemExit(f"--gpus {args.gpus} and --multi-device {args.multi_device} disagree")
+    if world > 1:  # one process per GPU under torch.distributed.run
+        if args.multi_device:
+            raise SystemExit("--multi-device is the single-process path: do not launch it with WORLD_SIZE > 1")
+        if args.gpus not in (None, world):
+            raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        args.gpus = world
+        return 0
+    n = args.multi_device or (args.gpus if args.gpus and args.gpus > 1 else 0)
+    if n and visible < n:
+        raise SystemExit(f"--gpus {n} without a launcher drives {n} GPUs from this process "
+                         f"(rtw_render_multi), but only {visible} are visible: nothing measured")
+    args.gpus = max(1, n)
+    return n
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs to measure (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="jumpy-1080p", choices=sorted(CONFIGS))
@@ -205,6 +232,7 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    multi = resolve_gpus(args, world, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dev_id = local % max(1, torch.cuda.device_count())
@@ -223,7 +251,6 @@ def main() -> int:
         spp = args.spp
     scene = rtw.Scene()
     cam, bg = scene.preset(scene_name, rtw.camera_aspect(w, h), seed=SCENE_SEED)
-    multi = args.multi_device if world == 1 else 0
     scene.commit(device=-1 if multi else dev)
     rt = rtw.Raytracer(scene, cam, bg, w, h, spp, seed=RENDER_SEED)
 
@@ -249,6 +276,8 @@ def main() -> int:
     def render_frame():
         if multi:
             rt.render_multi(multi)  # blocking: renders, gathers over RCCL, copies the frame to the host
+            if timing_multi is not None:
+                timing_multi.append(scene.multi_times())
             return
         if world == 1 and launches == 1:  # one GPU: the whole frame straight into the image (rtw_render's path)
             rt.render_device(image.data_ptr(), dev, 0, 0, stream.cuda_stream)
@@ -293,6 +322,7 @@ def main() -> int:
 
     gev = None         # (start, end) events of the current step's all-gather (N > 1)
     gather_ev = []     # those of the timed steps
+    timing_multi = None  # rtw_render_multi_times of the timed steps (single-process multi-device path)
     # exact ray count + traversal counters of this rank's share (untimed, same seed => same work)
     st = rt.render_device(packed.data_ptr(), dev, ids.data_ptr(), n_mine, stream.cuda_stream,
                           flags=rtw.FLAG_COUNT_TRAVERSAL, want_stats=True)
@@ -334,6 +364,8 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if multi:
+        timing_multi = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         if world > 1:
@@ -391,6 +423,20 @@ def main() -> int:
                      "gather_ms_min_over_ranks": min(gm),
                      "note": "gather ms = all-gather on torch's stream, incl. waiting for the slowest rank; its "
                              "minimum over ranks (the slowest rank's) is the transfer cost"}
+    if multi and timing_multi:  # the same diagnosis for the single-process N-GPU path (rtw_render_multi)
+        dms = np.array([t[0] for t in timing_multi], dtype=np.float64)  # steps x devices
+        gms_m = float(np.mean([t[1] for t in timing_multi]))
+        dk = []  # path-kernel ms per frame of every device (the library's events on that device's stream)
+        for d in range(multi):
+            pkd = pk if d == 0 else scene.path_kernel_times(d)  # device 0's were read above
+            dk.append(round(float(sum(pkd)) / args.steps, 3) if pkd else None)
+        km = [round(float(x), 3) for x in dms.mean(axis=0)]
+        multi_gpu = {"device_kernel_ms_per_frame": dk, "device_render_ms_per_frame": km,
+                     "gather_ms_per_frame": round(gms_m, 3),
+                     "kernel_imbalance_max_over_min": round(max(km) / min(km), 4) if min(km) > 0 else None,
+                     "note": "render ms = path kernel + in-order reduction per device (HIP events on its stream); "
+                             "gather ms = device 0's stream from the end of its render to the last device's "
+                             "tiles (RCCL send/recv group), so it includes waiting for the slowest device"}
     n_launch = launches * passes
     # per launch of this rank (multi-device: device 0's launches, its 1/N share of the frame)
     roof = roofline(cnt, frame_kernel_ms / n_launch, n_launch, multi or world, traffic, issue)
@@ -430,6 +476,8 @@ def main() -> int:
         }
         if multi_gpu:
             out["multi_gpu"] = multi_gpu
+        if out["n_gpus"] != args.gpus:  # never print an N = 1 line for an N-GPU request
+            raise SystemExit(f"bench measured {out['n_gpus']} GPU(s) but --gpus {args.gpus} was requested")
         if n_dev == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, cam, bg, w, h, spp, args.cpu_budget)
         else:

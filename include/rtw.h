@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 4
+#define RTW_ABI_VERSION 5
 
 enum {
   RTW_OK = 0,
@@ -222,7 +222,8 @@ int rtw_progress_decode(const uint8_t* frame, size_t len, rtw_progress_msg* msg)
  * stream (two renders in flight on different streams would share them).  The first render of a
  * given size allocates the sample buffer (hipMalloc: not stream-capturable); later renders of the
  * same or a smaller size only enqueue.  Without stats, a traversal fault of this render surfaces at
- * the next call (rtw_render_status). */
+ * the first rtw_render* call that starts after this render has COMPLETED (the check reads the device's
+ * host-mapped error word without waiting), or at rtw_render_status, which waits. */
 int rtw_render_device(rtw_scene* s, int device, const rtw_camera* cam, const float background[3],
                       uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
                       const uint32_t* d_tile_ids, uint32_t n_tiles, float* d_out, void* stream,
@@ -236,11 +237,13 @@ int rtw_render_device_strided(rtw_scene* s, int device, const rtw_camera* cam, c
                               uint32_t first_tile, uint32_t tile_stride, uint32_t n_tiles, float* d_out,
                               void* stream, uint32_t flags, rtw_stats* stats);
 /* Errors of renders the caller did not wait for.  A path kernel whose BVH walk trips its guard (a
- * corrupt tree: the walk is bounded so every wave drains) sets the device's host-mapped error word.
- * It is reported, and cleared, as RTW_EINVAL by the next rtw_render* call on that device (before it
- * enqueues), by rtw_path_kernel_times, by any call with stats, and by this function, which first
- * waits for all work on the device (hipDeviceSynchronize).  RTW_OK = every frame rendered so far on
- * `device` (-1: the first copy) is valid. */
+ * corrupt tree: the walk is bounded, and the first trip closes the path queue, so the grid drains after
+ * about one trip per wave) sets the device's host-mapped error word.  It is reported, and cleared, as
+ * RTW_EINVAL by the first rtw_render* call on that device that starts after the faulting render has
+ * completed (checked before it enqueues, without waiting: a call made while the faulting kernel still
+ * runs passes, and a later one reports it), by rtw_path_kernel_times and any call with stats (both wait
+ * first), and by this function, which first waits for all work on the device (hipDeviceSynchronize).
+ * RTW_OK = every frame rendered so far on `device` (-1: the first copy) is valid. */
 int rtw_render_status(rtw_scene* s, int device);
 /* Test hook: overwrite the device copy's first two BVH nodes with a cycle, so that every render of it
  * trips the traversal guard (tests/test_gpu_parity.py).  The scene stays unusable on that device. */
@@ -260,6 +263,13 @@ int rtw_diag_corrupt_bvh(rtw_scene* s, int device);
 int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const float background[3], uint32_t w,
                      uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, float* out_rgb_sum,
                      rtw_stats* stats);
+/* Timing of the scene's last rtw_render_multi call (a scaling run's diagnosis: load imbalance against
+ * gather cost): device_ms[d] = device d's render (path kernel + in-order reduction, HIP events on its
+ * stream) for d < min(cap, n); *gather_ms (may be NULL) = device 0's stream time from the end of its own
+ * render to the arrival of every device's tiles (the RCCL send/recv group, so it includes waiting for the
+ * slowest device; 0 for one device).  Returns n (0 before the first call).  Host only, no wait.
+ * (No reference counterpart: a benchmark hook beside rtw_render_multi.) */
+int rtw_render_multi_times(const rtw_scene* s, float* device_ms, uint32_t cap, float* gather_ms);
 
 /* The frame partition rtw_render_multi (and bench.py's one-process-per-GPU path) uses: the 8x8 tiles
  * of a w x h frame dealt round-robin to n_parts parts; part p gets tiles p, p + n, p + 2n, ...

@@ -129,6 +129,7 @@ _SIGS = {
     "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
     "rtw_render_multi": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.c_uint32, C.c_uint64, _F, C.POINTER(rtw_stats)]),
+    "rtw_render_multi_times": (C.c_int, [C.c_void_p, _F, C.c_uint32, _F]),
     "rtw_tile_partition": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _U32, C.c_uint32, _U32]),
     "rtw_render_stream": (C.c_int, [C.c_void_p, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_uint64, C.c_uint32, PIXEL_SINK, C.c_void_p,
@@ -156,7 +157,7 @@ EXPORTED_SYMBOLS = tuple(_SIGS)
 _lib = None
 
 
-ABI_VERSION = 4  # include/rtw.h RTW_ABI_VERSION
+ABI_VERSION = 5  # include/rtw.h RTW_ABI_VERSION
 
 
 def lib() -> C.CDLL:
@@ -404,6 +405,14 @@ class Scene:
         if n < 0:
             _check(n)
         return [float(buf[q]) for q in range(n)]
+
+    def multi_times(self, max_n: int = 64):
+        """(per-device render ms, device 0's gather ms) of the last rtw_render_multi call on this scene."""
+        buf, g = (C.c_float * max_n)(), C.c_float()
+        n = lib().rtw_render_multi_times(self._p, buf, max_n, C.byref(g))
+        if n < 0:
+            _check(n)
+        return [float(buf[q]) for q in range(min(n, max_n))], float(g.value)
 
     def render_status(self, device: int = -1) -> None:
         """Wait for the device and raise if a render since the last check tripped the traversal guard."""

@@ -140,7 +140,6 @@ struct Builder {
     memset(&p, 0, sizeof p);
     p.type_inst = PT_RECT_XY + axis;
     p.q0[0] = a0; p.q0[1] = a1; p.q0[2] = b0; p.q0[3] = b1; p.q1[0] = k;
-    if (!(fabsf(k) < 0x1p62f)) f.rect_k_small = 0;  // the kernel's reciprocal rect test then divides
     p.mat = mat;
     Box b;
     float lo[3], hi[3];
@@ -526,8 +525,10 @@ uint16_t h_round(double x, bool up) {
   return h_of_key(lo);
 }
 bool h_subnormal(uint16_t h) { return ((h >> 10) & 31) == 0 && (h & 1023) != 0; }
-// outward-rounded f16 offsets from a normal-or-zero f16 origin: no subnormal operand reaches the kernel
-void half_node(const DevNode4& n, DevNode4h& o) {
+// outward-rounded f16 offsets from a normal-or-zero f16 origin: no subnormal operand reaches the kernel.
+// false when a child's lower bound is below -65504: the origin would round down to -inf, every offset on
+// that axis would be +inf and the planes NaN (the caller then builds no half-precision table)
+bool half_node(const DevNode4& n, DevNode4h& o) {
   memset(&o, 0, sizeof o);
   const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
   const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
@@ -536,6 +537,7 @@ void half_node(const DevNode4& n, DevNode4h& o) {
     double mn = INFINITY;
     for (int k = 0; k < 4; ++k)
       if (n.lo_x[k] <= n.hi_x[k]) mn = std::min(mn, (double)lo[a][k]);
+    if (mn < -65504.0) return false;
     uint16_t org = mn == INFINITY ? 0 : h_round(mn, false);
     if (h_subnormal(org)) org = (org & 0x8000) ? 0x8400 : 0;  // -2^-14 or +0: still <= mn
     o.origin[a] = org;
@@ -555,6 +557,7 @@ void half_node(const DevNode4& n, DevNode4h& o) {
     }
   }
   for (int k = 0; k < 4; ++k) o.code[k] = (uint16_t)n.code[k];
+  return true;
 }
 
 bool texture_reads_uv(const Scene& s, uint32_t t, int guard = 0) {
@@ -825,7 +828,11 @@ int flatten(Scene& s) {
       }
     if (f.codes16) {
       f.nodes4h.resize(f.nodes4.size());
-      for (size_t q = 0; q < f.nodes4.size(); ++q) half_node(f.nodes4[q], f.nodes4h[q]);
+      for (size_t q = 0; q < f.nodes4.size(); ++q)
+        if (!half_node(f.nodes4[q], f.nodes4h[q])) {  // bounds beyond f16: the f32 table only
+          f.nodes4h.clear();
+          break;
+        }
     }
   }
   // feature set (selects the specialised kernel)

@@ -42,12 +42,19 @@
 namespace rtw {
 namespace dev {
 
-#ifndef RTW_SPH_RCP
-#define RTW_SPH_RCP 1  // sphere roots by Markstein's correction from a per-traversal RN(1 / |d|^2)
+// Compile-time switches.  The product build sets none of them.  Only these remain, and none changes a
+// result: RTW_NT_SAMPLES (0 = the sample buffer written / read with plain accesses; an A/B knob) and the
+// COUNT-build lane diagnostics RTW_LANE_DIAG / RTW_UNI_DIAG.  RTW_DIAG_ONE_TRIP (a timing diagnostic that is
+// NOT the reference's distribution) refuses to compile unless RTW_ALLOW_NON_REFERENCE is set as well, so no
+// product build can carry it.  Round 3's equivalence switches (sphere-root / unit() reciprocals, the
+// precomputed Dielectric ratios, start_path's LDS operands, select-form rect tests) are the only code now;
+// the dropped experiments (per-chain rect reciprocals, the xoroshiro64+ output) are deleted.
+#if defined(RTW_DIAG_ONE_TRIP) && !defined(RTW_ALLOW_NON_REFERENCE)
+#error "RTW_DIAG_ONE_TRIP changes the sampled distribution (not the reference's): diagnostic builds only"
 #endif
-
-#ifndef RTW_DIEL_PRE
-#define RTW_DIEL_PRE 1  // Dielectric 1 / ir and r0 precomputed by the flattener (DevShade::a)
+#if defined(RTW_RNG_PLUS) || defined(RTW_RECT_RCP) || defined(RTW_SPH_RCP) || defined(RTW_FAST_RCP) || \
+    defined(RTW_DIEL_PRE) || defined(RTW_START_LDS) || defined(RTW_RECT_SELECT)
+#error "removed compile-time switch (round 4): the kernel has one code path for it"
 #endif
 
 constexpr float TMIN = 0.001f;  // lib.rs:102
@@ -91,22 +98,8 @@ __device__ __forceinline__ float sqrt_rn(float x) {  // = sqrtf(x) for every x
   if (__builtin_expect(!(x >= 0x1p-96f && x < INFINITY), 0)) r = sqrtf(x);
   return r;
 }
-#ifndef RTW_FAST_RCP
-#define RTW_FAST_RCP 1  // IEEE divisions by Markstein's correction from rcp_rn (below): unit(), normals, tris
-#endif
-#ifndef RTW_START_LDS
-#define RTW_START_LDS 1  // start_path's kernel-uniform operands from an LDS copy (StartArgs)
-#endif
 #ifndef RTW_NT_SAMPLES
 #define RTW_NT_SAMPLES 1  // the sample buffer written with non-temporal stores
-#endif
-#ifndef RTW_RECT_SELECT
-#define RTW_RECT_SELECT 1  // rect tests and test_prim's accept as selects (kernels without triangles)
-#endif
-#ifndef RTW_RECT_RCP
-// list-mode rect tests from per-chain reciprocals (cand_rect_rcp): exact, but measured slower on cornell-800
-// (34.6k vs 35.5k Mrays/s with START_LDS; profiles/r03/experiments): off
-#define RTW_RECT_RCP 0
 #endif
 __device__ __forceinline__ bool near_zero(V3 a) {                                   // vec3.rs:133-138
   return fabsf(a.x) < 1e-8f && fabsf(a.y) < 1e-8f && fabsf(a.z) < 1e-8f;
@@ -133,11 +126,7 @@ __device__ __forceinline__ uint64_t xoro_seed(uint64_t h) { return h ? h : 0x9E3
 // multiply: 3 quarter-rate VALU ops)
 __device__ __forceinline__ uint32_t rng_next(uint64_t& s) {
   uint32_t s0 = (uint32_t)s, s1 = (uint32_t)(s >> 32);
-#if RTW_RNG_PLUS
-  const uint32_t result = s0 + s1;
-#else
   const uint32_t result = s0 * 0x9E3779BBu;
-#endif
   s1 ^= s0;
   s0 = __builtin_amdgcn_alignbit(s0, s0, 6) ^ s1 ^ (s1 << 9);  // rotl(s0, 26)
   s1 = __builtin_amdgcn_alignbit(s1, s1, 19);                   // rotl(s1, 13)
@@ -377,15 +366,11 @@ __device__ __forceinline__ float div_rcp(float x, float b, float y, bool b_ok) {
 // vec3.rs:85-87 unit_vector: a / |a|.  |a| = sqrt_rn (IEEE sqrt); the three divisions share the divisor, so
 // one rcp_rn and three corrections; |a.k| <= |a| needs no numerator guard.
 __device__ __forceinline__ V3 unit(V3 a) {
-#if RTW_FAST_RCP
   const float s = sqrt_rn(len2(a));
   const float y = rcp_rn_fast(s);
   V3 r = mk(div_by_recip(a.x, s, y), div_by_recip(a.y, s, y), div_by_recip(a.z, s, y));
   if (__builtin_expect(!recip_div_ok(s), 0)) r = divs(a, s);
   return r;
-#else
-  return divs(a, sqrtf(len2(a)));
-#endif
 }
 
 // ---- candidate t of one primitive (independent of t_max; -1 = miss)
@@ -410,11 +395,7 @@ struct SphRcp { float a, ya; bool ok; };
 __device__ __forceinline__ SphRcp sph_rcp(const Ray& r) {
   SphRcp q;
   q.a = len2(r.d);
-#if RTW_FAST_RCP
   q.ya = rcp_rn_fast(q.a);  // = 1.0f / a inside the guarded range below (outside it sph_div divides)
-#else
-  q.ya = 1.0f / q.a;
-#endif
   q.ok = q.a >= 0x1p-60f && q.a <= 0x1p60f;
   return q;
 }
@@ -466,51 +447,12 @@ __device__ __forceinline__ float cand_rect(const Ray& r, const float* q0, float 
   if (x < q0[0] || x > q0[1] || y < q0[2] || y > q0[3]) return -1.0f;
   return t;
 }
-// The rect test with the divisor's reciprocal computed once per wrapper chain (RectRcp: the object-space
-// direction's three components) instead of one IEEE division per rect: t = (k - o_k) / d_k by Markstein's
-// correction (3 VALU), the IEEE quotient wherever d_k is in [2^-60, 2^60] and |k - o_k| < 2^64.  The guard
-// is settled per chain too: |o_k| < 2^62 here and every rect's |k| < 2^62 (DevScene::rect_k_small, checked
-// by the flattener) bound the numerator.  A failed guard is stored as y = NaN (no lane masks to keep live:
-// the list-mode kernel is short of SGPRs), which makes the corrected quotient NaN, and those lanes divide.
-struct RectRcp {
-  float y[3];  // RN(1 / d.x), RN(1 / d.y), RN(1 / d.z), or NaN where the guard fails
-};
-__device__ __forceinline__ RectRcp rect_rcp(const Ray& r, uint32_t k_small) {
-  const float d[3] = {r.d.x, r.d.y, r.d.z}, o[3] = {r.o.x, r.o.y, r.o.z};
-  RectRcp q;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const bool ok = k_small && recip_div_ok(d[a]) && fabsf(o[a]) < 0x1p62f;
-    q.y[a] = ok ? rcp_rn_fast(d[a]) : __builtin_nanf("");
-  }
-  return q;
-}
-template <int AXIS>  // 0 XY, 1 XZ, 2 YZ — rectangular.rs:33-41, :84-92, :135-143
-__device__ __forceinline__ float cand_rect_rcp(const Ray& r, const float* q0, float k, const RectRcp& rr) {
-  const float o_k = AXIS == 0 ? r.o.z : (AXIS == 1 ? r.o.y : r.o.x);
-  const float d_k = AXIS == 0 ? r.d.z : (AXIS == 1 ? r.d.y : r.d.x);
-  constexpr int KA = AXIS == 0 ? 2 : (AXIS == 1 ? 1 : 0);
-  const float o_a = AXIS == 2 ? r.o.y : r.o.x, d_a = AXIS == 2 ? r.d.y : r.d.x;
-  const float o_b = AXIS == 0 ? r.o.y : r.o.z, d_b = AXIS == 0 ? r.d.y : r.d.z;
-  const float n = k - o_k;
-  float t = div_by_recip(n, d_k, rr.y[KA]);  // finite wherever the guard held (n and y finite)
-  if (__builtin_expect(t != t, 0)) t = n / d_k;
-  if (t < TMIN) return -1.0f;
-  float x = o_a + t * d_a;
-  float y = o_b + t * d_b;
-  if (x < q0[0] || x > q0[1] || y < q0[2] || y > q0[3]) return -1.0f;
-  return t;
-}
 struct TriUV { float t, u, v; };
 __device__ __forceinline__ TriUV tri_solve(const Ray& r, const float* q) {  // triangular.rs:98-118
   V3 a = mk(q[0], q[1], q[2]), ab = mk(q[3], q[4], q[5]), ac = mk(q[6], q[7], q[8]);
   V3 n = mk(q[9], q[10], q[11]);
   float det = -dot(r.d, n);
-#if RTW_FAST_RCP
   float inv = rcp_rn(det);  // triangular.rs:105 `1.0 / determinant`, the IEEE reciprocal
-#else
-  float inv = 1.0f / det;
-#endif
   V3 ao = sub(r.o, a);
   V3 aoxd = cross(ao, r.d);
   TriUV o;
@@ -641,8 +583,7 @@ __device__ __forceinline__ void test_sphere32(const DevScene& S, uint32_t pi, fl
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
 template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
 __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const Ray& wr, Best& b,
-                                          uint32_t* cnt, uint64_t seg, const SphRcp* rq = nullptr,
-                                          const RectRcp* rr = nullptr) {
+                                          uint32_t* cnt, uint64_t seg, const SphRcp* rq = nullptr) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
   // sphere-only worlds: a static sphere is tested as a moving one with c1 - c0 = 0 (c0 + time * 0 is
   // c0 up to the sign of a zero coordinate, which changes neither the decision nor t: the zero only
@@ -666,7 +607,7 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
   const uint32_t type = meta.x & 0xffu, inst = meta.x >> 8;
   // rect tests and the accept as selects instead of exec-mask branches (RTW_RECT_SELECT) in the kernels
   // without triangles: cornell-800 +6.7%; the triangle kernels lost 0.6-1.4% (profiles/r03/experiments, u1)
-  constexpr bool SEL = RTW_RECT_SELECT && !(FEAT & F_TRI);
+  constexpr bool SEL = !(FEAT & F_TRI);
   // object-space ray of the prim's wrapper chain; in BVH leaves recomputed per test (a few
   // flops) rather than cached, which keeps 8 VGPRs free for occupancy
   Ray lr = wr;
@@ -689,15 +630,9 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     t = cand_medium<FEAT>(S, lr, P, meta.y, meta.w, seg);
   } else if (FEAT & F_RECT) {
     const float k = q1v.x;
-    if (rr) {  // LOCAL: rr holds the reciprocals of this very ray's direction
-      if (type == PT_RECT_XY) t = cand_rect_rcp<0>(lr, q0, k, *rr);
-      else if (type == PT_RECT_XZ) t = cand_rect_rcp<1>(lr, q0, k, *rr);
-      else if (type == PT_RECT_YZ) t = cand_rect_rcp<2>(lr, q0, k, *rr);
-    } else {
-      if (type == PT_RECT_XY) t = cand_rect<0, SEL>(lr, q0, k);
-      else if (type == PT_RECT_XZ) t = cand_rect<1, SEL>(lr, q0, k);
-      else if (type == PT_RECT_YZ) t = cand_rect<2, SEL>(lr, q0, k);
-    }
+    if (type == PT_RECT_XY) t = cand_rect<0, SEL>(lr, q0, k);
+    else if (type == PT_RECT_XZ) t = cand_rect<1, SEL>(lr, q0, k);
+    else if (type == PT_RECT_YZ) t = cand_rect<2, SEL>(lr, q0, k);
   }
   if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }  // media: total only
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
@@ -772,27 +707,21 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
     uint32_t cur = 0;
     Ray lr = r;
-    // rect worlds: the reciprocals of the chain's direction once per chain, not a division per rect
-    constexpr bool RR = (FEAT & F_RECT) && RTW_RECT_RCP;
-    RectRcp rr;
-    if constexpr (RR) rr = rect_rcp(lr, S.rect_k_small);
     for (uint32_t k = 0; k < S.n_always; ++k) {
       const uint32_t pi = uload(S.always + k);
       const uint32_t inst = uload(&S.prims[pi].type_inst) >> 8;
       if (inst != cur) {
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
         cur = inst;
-        if constexpr (RR) rr = rect_rcp(lr, S.rect_k_small);
       }
-      test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg, nullptr, RR ? &rr : nullptr);
+      test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg);
     }
   } else {
     constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
     SphRcp rq;
-    if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
+    if constexpr (SPH_ONLY) rq = sph_rcp(r);
     for (uint32_t k = 0; k < S.n_always; ++k)
-      test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg,
-                                          (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
+      test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
   }
   // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR
   // across the whole loop and spilled it
@@ -836,7 +765,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   constexpr bool CODES = K16 || HN;  // leaves are 16-bit codes (the 32-bit walk keeps them sign-extended)
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
-  if constexpr (SPH_ONLY && RTW_SPH_RCP) rq = sph_rcp(r);
+  if constexpr (SPH_ONLY) rq = sph_rcp(r);
   // triangle-only BVH (DevScene::bvh_tri): the leaves' common object-space ray, once per call
   Ray tri_ray = r;
   if constexpr ((FEAT & F_TRI) != 0) {
@@ -1070,7 +999,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         for (int32_t k = 0; k < n; ++k) test_tri_leaf<COUNT>(S, (uint32_t)(first + k), tri_ray, ts.b, cnt);
       } else {
         for (int32_t k = 0; k < n; ++k)
-          test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, (SPH_ONLY && RTW_SPH_RCP) ? &rq : nullptr);
+          test_prim<COUNT, FEAT>(S, (uint32_t)(first + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
       }
       ts.pend = 0;
     }
@@ -1079,6 +1008,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
     if (done == __ballot(1) || (uint32_t)__popcll(done) >= quota) return;
   }
   *err = 1u;  // a guard tripped: end this traversal (miss) and report (a vector store to host memory)
+  ts.b.prim = -2;  // the path kernel drains the grid (see its miss branch)
   ts.node = -1;
   ts.sp = 0;
   ts.pend = 0;
@@ -1132,14 +1062,10 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     const float4 q0 = geo(0), q1 = geo(1), q2 = geo(2);
     V3 c = type == PT_SPHERE ? mk(q0.x, q0.y, q0.z) : center_at(q0, q1, PP, S.msphere_unit, lr.time);
     const float rad = q2.z;  // r (q0.w holds r * r)
-#if RTW_FAST_RCP
     // spherical.rs:49 (p - c) / r by the corrections from RN(1 / r), computed once by the flattener (q2.w)
     const V3 pc = sub(h.p, c);
     const bool ok = recip_div_ok(rad);
     outward = mk(div_rcp(pc.x, rad, q2.w, ok), div_rcp(pc.y, rad, q2.w, ok), div_rcp(pc.z, rad, q2.w, ok));
-#else
-    outward = divs(sub(h.p, c), rad);
-#endif
     if ((FEAT & F_UV) && (shade_kind & (1u << 12))) sphere_uv(outward, h.u, h.v);
   } else if ((FEAT & F_TRI) && type == PT_TRI) {
     const TriUV s{b.t, b.u, b.v};  // tri_solve's values from the winning test (the same ray and operands)
@@ -1300,11 +1226,7 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
   return mk(0.f, 0.f, 0.f);
 }
 
-__device__ __forceinline__ float schlick_r0(float ref_idx) {  // material.rs:109-110
-  const float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
-  return r0 * r0;
-}
-__device__ __forceinline__ float reflectance(float cosine, float r0) {  // material.rs:108-112, r0 = schlick_r0
+__device__ __forceinline__ float reflectance(float cosine, float r0) {  // material.rs:108-112, r0 precomputed (DevShade::a)
   float x = 1.0f - cosine;
   float x2 = x * x;
   return r0 + (1.0f - r0) * (x * (x2 * x2));  // powi(5) as LLVM expands it
@@ -1428,7 +1350,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
   // reload a v_readlane: cornell-800 +6%, jumpy +0.8%); the mesh variants regenerate paths every ~2
   // segments and lost 5-7% to the LDS reads' latency, so they keep the kernel arguments
-  constexpr bool SLDS = RTW_START_LDS && !(FEAT & F_TRI);
+  constexpr bool SLDS = !(FEAT & F_TRI);
   __shared__ StartArgs start_lds[SLDS ? 1 : 0 + 1];
   StartArgs sa_reg;
   if constexpr (SLDS) {
@@ -1558,6 +1480,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     if (b.prim < 0) {  // lib.rs:102-105
       L = mul(T, bg);
       done = true;
+      if (__builtin_expect(b.prim == -2, 0)) {
+        // trace_run tripped its guard (a corrupt tree; the frame is invalid and reported): close the path queue
+        // for every wave and empty this wave's id pool, so the grid drains after about one trip per wave
+        // instead of one per 64 paths (a trip is 2^20 node-loop iterations)
+        atomicMax(a.queue, (unsigned long long)P);
+        pool[0] = pool[1];
+      }
     } else {
       // the prim's shading record is loaded as soon as the winner is known, beside its geometry
       // (one load instead of the prim -> material -> texture -> checker-child chain)
@@ -1613,15 +1542,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           dir = add(reflect(ud, h.n), scale(rs, sh.param));
           done = !(dot(dir, h.n) > 0.0f);  // absorbed: emitted() is black
         } else if (!iso && (FEAT & F_DIEL)) {  // Dielectric, material.rs:116-142
-#if RTW_DIEL_PRE
           // 1 / ir (material.rs:120) and Schlick's r0 (:108-112) for both ratios: the same f32
           // operations, evaluated once by the flattener (DevShade::a)
           const float ratio = h.front ? sh.a[0] : sh.param;
           const float r0 = h.front ? sh.a[1] : sh.a[2];
-#else
-          const float ratio = h.front ? 1.0f / sh.param : sh.param;
-          const float r0 = schlick_r0(ratio);
-#endif
           const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
           const float sin_t = sqrtf(1.0f - cos_t * cos_t);
           const bool cannot = (ratio * sin_t) > 1.0f;
@@ -1832,7 +1756,6 @@ int upload(Scene& s, int device) {
     c.scene.n_insts = (uint32_t)f.insts.size();
     c.scene.msphere_unit = f.msphere_unit;
     c.scene.uni_inst = f.uni_inst;
-    c.scene.rect_k_small = f.rect_k_small;
     c.scene.bvh_tri = f.bvh_tri;  // knob RTW_TRI_LEAF (rtw_flatten.cpp)
     c.scene.tri_inst = f.tri_inst;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
@@ -1858,6 +1781,8 @@ void release(Scene& s) {
     if (c.spill) hipFree(c.spill);
     for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids}) free_buf(*b);
     for (void* e : c.ev)
+      if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
+    for (void* e : c.gev)
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
     if (c.stream) hipStreamDestroy(static_cast<hipStream_t>(c.stream));
     for (auto& e : c.kev)
@@ -1944,7 +1869,7 @@ static Variant pick5(uint32_t need, bool half = false) {
 }
 template <bool C>
 static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
-                           bool codes16) {
+                           bool codes16, bool has_half) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -1954,8 +1879,9 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
   // +3.3% (its 2,226-node tree), cow-1080p -6.5% (1,591 nodes), jumpy-1080p -4.9% (LDS nodes).  So by
   // default only mesh trees of >= 2048 node4s use them; knob RTW_HALF_NODES 1 = wherever built, 0 = never.
   const int half_knob = env_int("RTW_HALF_NODES", -1);
-  const bool half = codes16 && (half_knob > 0 || (half_knob < 0 && n_nodes >= 2048));
-  const bool half_lds = codes16 && half_knob > 0;
+  // (no half-precision table when a bound is beyond f16's range: rtw_flatten.cpp half_node)
+  const bool half = has_half && (half_knob > 0 || (half_knob < 0 && n_nodes >= 2048));
+  const bool half_lds = has_half && half_knob > 0;
   if (list && !env_int("RTW_GENERIC", 0)) {
     // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
     // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
@@ -2022,8 +1948,9 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
 static Variant path_kernel_variant(bool count, const Flat& f) {
   const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
   const bool list = f.nodes4.empty();
-  return count ? pick_kernel<true>(feat, need, list, nn, need4, f.codes16)
-               : pick_kernel<false>(feat, need, list, nn, need4, f.codes16);
+  const bool hh = f.codes16 && !f.nodes4h.empty();
+  return count ? pick_kernel<true>(feat, need, list, nn, need4, f.codes16, hh)
+               : pick_kernel<false>(feat, need, list, nn, need4, f.codes16, hh);
 }
 
 static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {

@@ -11,8 +11,10 @@
 //
 // RCCL is opened at the first render over more than one device (dlopen of librccl.so.1, or the file
 // named by RTW_RCCL_LIB), so the rest of the library -- rtw_render_multi(n_gpus = 1) included -- does
-// not depend on it.  The loader and the communicator cache are guarded by one mutex: host threads may
-// call rtw_render_multi concurrently on different scenes.
+// not depend on it.  The loader and the communicator cache are guarded by one mutex, and every use of a
+// clique's communicators (ncclGroupStart .. ncclGroupEnd) by that clique's own mutex, so host threads may
+// call rtw_render_multi concurrently on different scenes: RCCL communicators are not thread-safe, and two
+// interleaved grouped send/recv sequences on the same communicators could deadlock.
 #include <dlfcn.h>
 #include <stdlib.h>
 #include <hip/hip_runtime_api.h>
@@ -83,6 +85,7 @@ Rccl& rccl() {
 struct Clique {
   int n = 0;
   std::vector<ncclComm_t> comms;
+  std::mutex mu;  // held from ncclGroupStart through ncclGroupEnd of one gather
 };
 std::vector<std::unique_ptr<Clique>>& cliques() {  // callers hold rccl_mutex()
   static std::vector<std::unique_ptr<Clique>> c;
@@ -100,11 +103,11 @@ std::vector<std::unique_ptr<Clique>>& cliques() {  // callers hold rccl_mutex()
     if (r_ != ncclSuccess) return fail(RTW_ENODEV, "%s: %s", what, rccl().error_string(r_)); \
   } while (0)
 
-int get_clique(int n, std::vector<ncclComm_t>** out) {
+int get_clique(int n, Clique** out) {
   std::lock_guard<std::mutex> lock(rccl_mutex());
   for (auto& c : cliques())
     if (c->n == n) {
-      *out = &c->comms;
+      *out = c.get();
       return RTW_OK;
     }
   Rccl& r = rccl();
@@ -115,7 +118,7 @@ int get_clique(int n, std::vector<ncclComm_t>** out) {
   std::vector<int> devs(n);
   for (int d = 0; d < n; ++d) devs[d] = d;
   NCCLOK(r.comm_init_all(c->comms.data(), n, devs.data()), "ncclCommInitAll");
-  *out = &c->comms;
+  *out = c.get();
   cliques().push_back(std::move(c));
   return RTW_OK;
 }
@@ -197,13 +200,16 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
     memset(&st1, 0, sizeof st1);
     if (int e = collect_stats(c, st, e0[0], e1[0], (uint64_t)w * h * spp, &st1)) return e;
     HIPOK(hipMemcpy(out, c.image.p, frame_bytes, hipMemcpyDeviceToHost), "hipMemcpy(image)");
+    s->s.multi_ms.assign(1, (float)st1.kernel_ms);
+    s->s.multi_gather_ms = 0.0f;
     st1.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (stats) *stats = st1;
     return RTW_OK;
   }
 
-  std::vector<ncclComm_t>* comms = nullptr;
-  if (int e = get_clique(n, &comms)) return e;
+  Clique* clique = nullptr;
+  if (int e = get_clique(n, &clique)) return e;
+  const std::vector<ncclComm_t>* comms = &clique->comms;
   const Rccl& r = rccl();  // loaded by get_clique; never changes afterwards
   const uint32_t per = (nt + (uint32_t)n - 1) / (uint32_t)n;  // padded tiles per device
   const size_t slot_floats = (size_t)per * 64 * 3;
@@ -237,23 +243,37 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   HIPOK(hipMemcpyAsync(c0.gather_ids.p, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st0),
         "hipMemcpyAsync(gather ids)");
   float* gathered = static_cast<float*>(c0.gathered.p);
-  NCCLOK(r.group_start(), "ncclGroupStart");
-  for (int d = 0; d < n; ++d) {
-    hipStream_t st = static_cast<hipStream_t>(cp[d]->stream);
-    const ncclResult_t a = r.send(cp[d]->packed.p, slot_floats, ncclFloat32, 0, (*comms)[d], st);
-    if (a != ncclSuccess) {
-      r.group_end();
-      return fail(RTW_ENODEV, "ncclSend: %s", r.error_string(a));
+  // device 0's gather time: its stream from the end of its own render to the last tile's arrival (so it
+  // includes waiting for the slowest device), rtw_render_multi_times
+  for (void*& e : c0.gev)
+    if (!e) {
+      hipEvent_t x;
+      HIPOK(hipEventCreate(&x), "hipEventCreate");
+      e = x;
     }
-  }
-  for (int d = 0; d < n; ++d) {
-    const ncclResult_t a = r.recv(gathered + (size_t)d * slot_floats, slot_floats, ncclFloat32, d, (*comms)[0], st0);
-    if (a != ncclSuccess) {
-      r.group_end();
-      return fail(RTW_ENODEV, "ncclRecv: %s", r.error_string(a));
+  HIPOK(hipEventRecord(static_cast<hipEvent_t>(c0.gev[0]), st0), "hipEventRecord");
+  {
+    std::lock_guard<std::mutex> lock(clique->mu);  // one grouped send/recv on these communicators at a time
+    NCCLOK(r.group_start(), "ncclGroupStart");
+    for (int d = 0; d < n; ++d) {
+      hipStream_t st = static_cast<hipStream_t>(cp[d]->stream);
+      const ncclResult_t a = r.send(cp[d]->packed.p, slot_floats, ncclFloat32, 0, (*comms)[d], st);
+      if (a != ncclSuccess) {
+        r.group_end();
+        return fail(RTW_ENODEV, "ncclSend: %s", r.error_string(a));
+      }
     }
+    for (int d = 0; d < n; ++d) {
+      const ncclResult_t a = r.recv(gathered + (size_t)d * slot_floats, slot_floats, ncclFloat32, d, (*comms)[0], st0);
+      if (a != ncclSuccess) {
+        r.group_end();
+        return fail(RTW_ENODEV, "ncclRecv: %s", r.error_string(a));
+      }
+    }
+    NCCLOK(r.group_end(), "ncclGroupEnd");
   }
-  NCCLOK(r.group_end(), "ncclGroupEnd");
+  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipEventRecord(static_cast<hipEvent_t>(c0.gev[1]), st0), "hipEventRecord");
   // 3. device 0 scatters the gathered tiles into the frame and copies it out
   HIPOK(hipSetDevice(0), "hipSetDevice");
   if (int e = enqueue_unpack(w, h, static_cast<uint32_t*>(c0.gather_ids.p), (uint32_t)all.size(), gathered,
@@ -263,6 +283,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
         "hipMemcpyAsync(image)");
   rtw_stats tot;
   memset(&tot, 0, sizeof tot);
+  std::vector<float> dev_ms(n);
   for (int d = 0; d < n; ++d) {
     HIPOK(hipSetDevice(d), "hipSetDevice");
     rtw_stats st;
@@ -270,11 +291,26 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
     if (int e = collect_stats(*cp[d], cp[d]->stream, e0[d], e1[d], 0, &st)) return e;
     tot.rays += st.rays;
     tot.kernel_ms = std::max(tot.kernel_ms, st.kernel_ms);  // the devices run concurrently
+    dev_ms[d] = (float)st.kernel_ms;
   }
+  float gms = 0.0f;
+  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipEventElapsedTime(&gms, static_cast<hipEvent_t>(c0.gev[0]), static_cast<hipEvent_t>(c0.gev[1])),
+        "hipEventElapsedTime(gather)");
+  s->s.multi_ms = dev_ms;
+  s->s.multi_gather_ms = gms;
   tot.paths = (uint64_t)w * h * spp;
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = tot;
   return RTW_OK;
+}
+
+int rtw_render_multi_times(const rtw_scene* s, float* device_ms, uint32_t cap, float* gather_ms) {
+  if (!s || (cap && !device_ms)) return fail(RTW_EINVAL, "NULL argument");
+  const std::vector<float>& v = s->s.multi_ms;
+  for (size_t d = 0; d < v.size() && d < cap; ++d) device_ms[d] = v[d];
+  if (gather_ms) *gather_ms = s->s.multi_gather_ms;
+  return (int)v.size();
 }
 
 }  // extern "C"

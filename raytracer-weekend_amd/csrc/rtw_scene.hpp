@@ -74,7 +74,6 @@ struct Flat {
   uint32_t features = 0;  // Feature bits actually used
   uint32_t msphere_unit = 1;  // every moving sphere has the shutter [+0, 1] (DevPrim::aux)
   uint32_t uni_inst = 0;      // the only instance, a single Translation (0 = none such)
-  uint32_t rect_k_small = 1;  // every rect's |k| < 2^62 (DevScene::rect_k_small)
   uint32_t bvh_tri = 0;       // every BVH leaf is a triangle of wrapper chain tri_inst (DevScene::bvh_tri)
   uint32_t tri_inst = 0;
   float uni_off[3] = {0, 0, 0};
@@ -109,6 +108,7 @@ struct DeviceCopy {
   DevBuf image, tiles, packed, gathered, gather_ids;
   void* ev[2] = {nullptr, nullptr};        // hipEvent_t pair timing rtw_render / multi calls
   void* stream = nullptr;                  // hipStream_t of rtw_render_multi on this device
+  void* gev[2] = {nullptr, nullptr};       // hipEvent_t pair around rtw_render_multi's gather (device 0)
 };
 
 struct Scene {
@@ -121,6 +121,10 @@ struct Scene {
   bool committed = false;
   Flat flat;
   std::vector<DeviceCopy> dev;
+  // the last rtw_render_multi call: per-device render ms (path kernel + in-order reduction) and device 0's
+  // gather ms (rtw_render_multi_times)
+  std::vector<float> multi_ms;
+  float multi_gather_ms = 0.0f;
   Scene() { nodes.push_back(Node{NK_LIST, {}}); }
 };
 

@@ -226,3 +226,30 @@ def test_half_nodes_contain_the_f32_boxes(rtw, name):
         ob = nh["origin"].view(np.uint16)
         assert not (((ob & 0x7C00) == 0) & ((ob & 0x3FF) != 0)).any()
     assert np.array_equal(nh["code"].astype(np.uint32), nd["code"])
+
+
+@pytest.mark.parametrize("offset,built", [(-1.0e5, False), (-6.0e4, True), (1.0e5, True)])
+def test_half_nodes_beyond_f16_range(rtw, offset, built):
+    """a child box whose lower bound is below -65504 would get an f16 origin of -inf (every offset
+    +inf, every plane NaN).  The flattener then builds no half-precision table (the kernels walk the f32
+    one); bounds above +65504 round outward to +inf offsets (conservative) and keep it."""
+    rng = np.random.default_rng(7)
+    s = rtw.Scene()
+    m = s.lambertian_solid((0.5, 0.5, 0.5))
+    n = 600
+    base = rng.uniform(-50, 50, (n, 1, 3)) + np.array([offset, 0.0, 0.0])
+    verts = (base + rng.uniform(-1, 1, (n, 3, 3))).astype(np.float32)
+    with s.bvh():
+        s.triangles(verts.reshape(-1), m)
+    _commit_anywhere(rtw, s)
+    nd, nh = s.nodes(), s.nodes_half()
+    assert len(nd) > 4
+    assert (len(nh) == len(nd)) == built
+    if built:
+        for ax in ("x", "y", "z"):
+            org = nh["origin"][:, "xyz".index(ax)].astype(np.float64)
+            assert np.all(np.isfinite(org)), ax
+            lo16 = nh[ax][:, 0, :4].astype(np.float64)
+            full = ~(nd["lo_x"] > nd["hi_x"])
+            with np.errstate(invalid="ignore"):
+                assert np.all((org[:, None] + lo16 <= nd["lo_" + ax])[full]), ax

@@ -108,6 +108,41 @@ def test_corrupt_bvh_fails_every_path(gpu, monkeypatch, knob):
     del good
 
 
+@pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0"])
+def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, monkeypatch, knob):
+    """after a guard trip the kernel closes the path queue and empties the wave's id pool, so a
+    large corrupt frame costs about one trip per wave, not one per 64 paths.  A 256x256x16 frame (16 K
+    64-path groups, ~1 K waves with work) must take at most 8x the time of an 8x8x1 frame (one wave, one
+    trip); without the drain every wave runs ~16 trips in a row."""
+    import time
+    torch = pytest.importorskip("torch")
+    if knob:
+        monkeypatch.setenv(*knob.split("="))
+    rtw = gpu
+    s, cam, bg = _sphere_cloud(rtw)
+    s.commit(device=0)
+    s.diag_corrupt_bvh(0)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def timed(w, h, spp):
+        out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
+        rt = rtw.Raytracer(s, cam, bg, w, h, spp, seed=1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rt.render_device(out.data_ptr(), 0, 0, 0, stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        with pytest.raises(rtw.RtwError):
+            s.render_status(0)
+        return dt
+
+    timed(8, 8, 1)  # warm-up (buffers, code objects)
+    small = timed(8, 8, 1)
+    big = timed(256, 256, 16)
+    print(f"corrupt frames: 8x8x1 {small:.3f} s, 256x256x16 {big:.3f} s")
+    assert big <= 8.0 * small + 0.5, (small, big)
+
+
 def test_render_multi_one_gpu_needs_no_rccl(gpu, monkeypatch):
     """rtw_render_multi over one device is rtw_render's path: it never opens RCCL, so it
     works with the RCCL library made unloadable, and equals rtw_render bit for bit."""

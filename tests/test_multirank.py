@@ -162,3 +162,82 @@ def test_strided_render_rejects_tiles_outside_the_frame(rtw):
         with pytest.raises(rtw.RtwError) as e:
             rt.render_device_strided(1, 0, first, stride, n)
         assert e.value.code == rtw.RTW_EINVAL
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rtw_bench_mod", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _args(**kw):
+    import argparse
+    d = dict(gpus=None, multi_device=0)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def test_bench_gpus_routing_without_launcher():
+    """`--gpus N` always means N.  Without a launcher, N > 1 goes to the single-process
+    rtw_render_multi(N) path when N GPUs are visible, and exits non-zero (no line) otherwise."""
+    b = _bench_module()
+    a = _args(gpus=8)
+    assert b.resolve_gpus(a, world=1, visible=8) == 8 and a.gpus == 8
+    a = _args()
+    assert b.resolve_gpus(a, world=1, visible=8) == 0 and a.gpus == 1  # default: the one-GPU path
+    a = _args(gpus=1)
+    assert b.resolve_gpus(a, world=1, visible=0) == 0 and a.gpus == 1
+    a = _args(multi_device=1)
+    assert b.resolve_gpus(a, world=1, visible=1) == 1 and a.gpus == 1
+    for kw, vis in ((dict(gpus=2), 1), (dict(gpus=8), 0), (dict(multi_device=4), 2), (dict(gpus=2, multi_device=4), 8),
+                    (dict(gpus=0), 8)):
+        with pytest.raises(SystemExit):
+            b.resolve_gpus(_args(**kw), world=1, visible=vis)
+
+
+def test_bench_gpus_routing_under_launcher():
+    b = _bench_module()
+    a = _args(gpus=4)
+    assert b.resolve_gpus(a, world=4, visible=8) == 0 and a.gpus == 4
+    a = _args()
+    assert b.resolve_gpus(a, world=2, visible=8) == 0 and a.gpus == 2
+    for kw in (dict(gpus=1), dict(gpus=8), dict(multi_device=4)):
+        with pytest.raises(SystemExit):
+            b.resolve_gpus(_args(**kw), world=4, visible=8)
+
+
+def test_bench_gpus_2_without_gpus_fails_loudly():
+    """`python bench.py --gpus 2` on a box without 2 visible GPUs (here: none) exits non-zero and prints no
+    bench line -- never a 1-GPU number for a 2-GPU request."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode != 0
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            assert "n_gpus" not in json.loads(line), line
+    assert "--gpus 2" in r.stderr
+
+
+def test_monument_per_rank_share_is_one_pass():
+    """configs[4] (monument 3840x2160x1024) over 8 GPUs: each rank's round-robin share is at most 2^32 paths, so
+    enqueue_render sizes its sample buffer once for the whole share and runs ONE path-kernel pass
+    (max_pass_paths = 2^32); on one GPU the frame takes two passes."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from conftest import load_rtw
+    T = load_rtw()
+    w, h, spp = 3840, 2160, 1024
+    per_slot = 64 * spp
+    slots_per_pass = (1 << 32) // per_slot
+    for n in (1, 2, 4, 8):
+        shares = [T.tile_partition(w, h, n, p)[1] for p in range(n)]
+        passes = [-(-k // slots_per_pass) for k in shares]
+        assert passes == [2 if n == 1 else 1] * n, (n, passes)
+        if n == 8:
+            assert max(shares) * per_slot * 12 < 13e9  # 12 B per path: ~12.7 GB per rank
