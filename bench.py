@@ -395,21 +395,34 @@ def main() -> int:
 
     value = frame_rays * args.steps / dt / 1e6
     # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +
-    # WRITE_SIZE, separate passes; scripts/gpu_profile.sh + scripts/prof_summary.py), if any
+    # WRITE_SIZE, separate passes; scripts/gpu_r04_evidence.sh + scripts/summarize_round.py), if any --
+    # attached only when it was measured on THIS library build (its lib_sha stamp), else null + the reason
+    sha = rtw.lib_sha()
+    evidence_notes = []
+
+    def same_build(d, path):
+        if d.get("lib_sha") == sha:
+            return True
+        evidence_notes.append(f"{path.relative_to(ROOT)} was measured on build {d.get('lib_sha') or 'unstamped'}, "
+                              f"the timed library is {sha}: not attached")
+        return False
+
     traffic, traffic_src = None, None
     tj = Path(args.traffic_json) if args.traffic_json else ROOT / "profiles" / f"pmc_{args.config}.json"
     if tj.exists() and not args.spp and not multi:
         d = json.loads(tj.read_text())
-        if d.get("launches_per_frame", 1) == launches and d.get("world", 1) == world:
+        if d.get("launches_per_frame", 1) == launches and d.get("world", 1) == world and same_build(d, tj):
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), str(tj.relative_to(ROOT))
-    # what bounds it: SQ counters of the same config (scripts/gpu_counters.sh + valu_summary.py)
+    # what bounds it: SQ counters of the same config and build (summarize_round.py)
     issue = None
     vj = ROOT / "profiles" / f"valu_{args.config}.json"
-    if vj.exists() and not args.spp:
+    if vj.exists() and not args.spp and not multi:
         d = json.loads(vj.read_text())
-        issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit",
-                                        "ta_busy", "td_busy", "lds_active", "lds_conflict_share")}
-        issue["source"] = str(vj.relative_to(ROOT))
+        if same_build(d, vj):
+            issue = {k: d.get(k) for k in ("valu_busy", "valu_lane_util", "wave_wait", "wave_issue", "l2_hit",
+                                            "ta_busy", "td_busy", "lds_active", "lds_conflict_share",
+                                            "tcp_hit", "vmem_rd_per_ray")}
+            issue["source"] = str(vj.relative_to(ROOT))
     multi_gpu = None
     if world > 1:  # per-rank kernel / gather time: imbalance vs gather cost (a scaling run's diagnosis)
         gms = sum(a.elapsed_time(b) for a, b in gather_ev) / len(gather_ev) if gather_ev else float("nan")
@@ -444,7 +457,8 @@ def main() -> int:
     out = None
     if rank == 0:
         n_dev = multi or world
-        roof.update({"traffic_source": traffic_src, "issue_counters": issue, "kernel": "path_kernel",
+        roof.update({"traffic_source": traffic_src, "issue_counters": issue, "lib_sha": sha,
+                     "evidence_notes": evidence_notes or None, "kernel": "path_kernel",
                      "kernel_ms_per_frame": round(frame_kernel_ms, 3), "kernel_launches_per_frame": n_launch,
                      "node_fetches_per_ray": round(cnt["node4"] / max(1, cnt["rays"]), 3),
                      "boxes_per_ray": round(cnt["boxes"] / max(1, cnt["rays"]), 3),

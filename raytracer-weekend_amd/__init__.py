@@ -160,6 +160,13 @@ _lib = None
 ABI_VERSION = 5  # include/rtw.h RTW_ABI_VERSION
 
 
+def lib_sha() -> str:
+    """First 16 hex digits of the SHA-256 of the library file this process loads (LIB_PATH): ties profiler
+    evidence under profiles/ to the build it was measured on (bench.py attaches it only on a match)."""
+    import hashlib
+    return hashlib.sha256(LIB_PATH.read_bytes()).hexdigest()[:16] if LIB_PATH.exists() else ""
+
+
 def lib() -> C.CDLL:
     """Load librtw_amd.so (fails loudly: there is no fallback path)."""
     global _lib

@@ -17,15 +17,17 @@
 // conservative (padded boxes + slack), so it changes which nodes are visited, never the answer.
 //
 // Kernel structure: path_kernel is PERSISTENT -- the grid is the resident capacity,
-// and each wave draws path ids from one global queue (2048 per atomic) into an LDS pool, hands them
-// to its idle lanes by ballot + mbcnt prefix (64 consecutive ids = one sample of one 8x8 tile), and
+// and each wave draws path ids from one global queue (RenderArgs::batch per atomic: 1024 in the
+// 1024-lane LDS-node and the list-mode kernels, 2048 elsewhere; knob RTW_BATCH) into an LDS pool, hands
+// them to its idle lanes by ballot + mbcnt prefix (64 consecutive ids = one sample of one 8x8 tile), and
 // loops: regenerate -> trace_begin (the always-tested list) -> trace_run (resumable BVH4 walk with
 // postponed leaves; returns once quota16/16 of the lanes are done) -> shade.  A finished path writes
 // its radiance to an ordered sample buffer that reduce_kernel sums per pixel in sample order.
-// Variants (pick_kernel): feature-specialised instantiations; the LDS-node kernel (512-lane
-// workgroups, the whole node table in LDS, sorted-push walk over 16-bit child codes) for sphere
-// worlds that fit; the global-node kernels (256-lane workgroups, 32-bit LDS stack) for meshes, with
-// half-precision nodes (DevNode4h) for large trees; BVH-less list-mode kernels for <= 32 primitives.
+// Variants (pick_kernel): feature-specialised instantiations; the LDS-node kernel for sphere worlds whose
+// tree fits (the whole node table in LDS, sorted-push walk over 16-bit child codes; by default 1024-lane
+// workgroups, 2 per CU at 8 waves/SIMD, with the paths' T / depth / id in LDS rows: DESIGN.md §3); the
+// global-node kernels (256-lane workgroups, 32-bit LDS stack) for meshes, with half-precision nodes
+// (DevNode4h) for large trees; BVH-less list-mode kernels for <= 32 primitives.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>

@@ -44,7 +44,15 @@ def main():
         d.mkdir(parents=True, exist_ok=True)
         lines = [l for l in (s / "bench.log").read_text().splitlines() if l.startswith("{")]
         (d / "bench.json").write_text(lines[-1] + "\n")
+        # every run of this config in the evidence call used the same in-tree library: its stamp, as the bench
+        # line saw it, goes into the published files (bench.py attaches them only to that build)
+        sha = json.loads(lines[-1])["roofline"].get("lib_sha")
+        for other in (s / "kt.log",):
+            js = [l for l in other.read_text().splitlines() if l.startswith("{")] if other.exists() else []
+            if js and json.loads(js[-1])["roofline"].get("lib_sha") != sha:
+                raise SystemExit(f"{other}: another build than {s / 'bench.log'}")
         shutil.copy(s / "kt" / "kt_kernel_stats.csv", d / "kernel_stats.csv")
+        rays = json.loads(lines[-1])["config"]["rays_per_frame"] / json.loads(lines[-1])["roofline"]["kernel_launches_per_frame"]
         pmc = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             f = s / f"pmc_{c}" / "pmc_counter_collection.csv"
@@ -55,10 +63,10 @@ def main():
                "hbm_bytes_per_launch": 2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"],
                "fetch_bytes_per_launch_raw": pmc["FETCH_SIZE"], "write_bytes_per_launch": pmc["WRITE_SIZE"],
                "correction": "FETCH_SIZE x2 (gfx950 counts 64 B per 128-B request), WRITE_SIZE as is; KiB -> B",
-               "source": str(d.relative_to(ROOT))}
+               "source": str(d.relative_to(ROOT)), "lib_sha": sha}
         (ROOT / "profiles" / f"pmc_{cfg}.json").write_text(json.dumps(pub, indent=1))
         c = {}
-        for i in (1, 2, 3, 4):
+        for i in (1, 2, 3, 4, 5):
             f = s / f"sq{i}" / "sq_counter_collection.csv"
             if not f.exists():
                 continue
@@ -82,8 +90,16 @@ def main():
                 # spent on bank conflicts (MI355X_MICROARCH.md §LDS)
                 "lds_active": round(c["SQ_LDS_IDX_ACTIVE"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4) if "SQ_LDS_IDX_ACTIVE" in c else None,
                 "lds_conflict_share": ratio("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"),
+                # vector L1 (TCP): hit share of its accesses (1 - requests it sends to L2 / accesses), and vector
+                # loads per ray (SQ_INSTS_VMEM_RD per wave instruction, 64 lanes each, over the frame's rays)
+                "tcp_hit": round(1.0 - c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"], 4)
+                if c.get("TCP_TOTAL_CACHE_ACCESSES_sum") and "TCP_TCC_READ_REQ_sum" in c else None,
+                "tcp_pending_stall_share": round(c["TCP_PENDING_STALL_CYCLES_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8), 4)
+                if "TCP_PENDING_STALL_CYCLES_sum" in c and c.get("GRBM_GUI_ACTIVE") else None,
+                "vmem_rd_per_ray": round(c["SQ_INSTS_VMEM_RD"] * 64 / rays, 3) if c.get("SQ_INSTS_VMEM_RD") and rays else None,
                 "counters": {k: round(v) for k, v in sorted(c.items())},
-                "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r02.sh)"}
+                "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r04_evidence.sh)",
+                "lib_sha": sha}
         (ROOT / "profiles" / f"valu_{cfg}.json").write_text(json.dumps(valu, indent=1))
         print(cfg, "pmc", pub["hbm_bytes_per_launch"], "valu_busy", valu["valu_busy"], "lane", valu["valu_lane_util"])
     subprocess.run([sys.executable, str(ROOT / "scripts" / "roofline.py"), str(dst)] + cfgs, check=True)
