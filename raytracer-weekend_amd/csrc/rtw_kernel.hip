@@ -1638,6 +1638,266 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   o[2] = z;
 }
 
+// ---- wavefront prototype (knob RTW_WAVEFRONT=1): the megakernel's loop split across
+// kernels by phase, so that every wave of a phase works on rays of that phase only.  Each iteration:
+//   wf_trace_kernel (persistent, LDS node table): its waves take items from this iteration's queues -- slots
+//     holding a scattered ray (rayq), then free slots (freeq), which start a new path (start_path, the path id
+//     from the same global dispenser as the megakernel) -- and trace them with the same resumable walk; a
+//     lane whose query is done stores (t, prim) and is refilled at once (no shading phase to wait for).
+//   wf_shade_kernel (one thread per item): the megakernel's shading body for the slot's hit; a finished path
+//     writes its sample and returns its slot to the next freeq, a scattered ray goes to the next rayq
+//     (wave-aggregated appends: one atomic per wave and queue).
+// Slot state lives in global memory (SoA, ~80 B per slot; RTW_WF_SLOTS slots, sized for the 256 MB
+// Infinity Cache).  Pixels depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
+struct WfArgs {
+  float4* ray_o;       // o.xyz, time
+  float4* ray_d;       // d.xyz, -
+  float4* thr;         // T.xyz, remaining depth (bits)
+  uint64_t* rng;       // the path's xoroshiro64* state
+  uint32_t* pid;       // path id within the pass
+  uint2* hit;          // (t bits, prim); prim -3: no path left for the slot, -4: its id was off the image
+  uint32_t* rayq[2];   // slots with a ray to trace (iteration parity p reads [p], shading appends to [1 - p])
+  uint32_t* freeq[2];  // slots to start a new path in
+  uint32_t* cnt;       // [0, 1] rayq counts, [2, 3] freeq counts, [4] trace item head
+  uint32_t n_slots;
+  uint32_t par;
+};
+
+#ifndef WF_OCC
+#define WF_OCC 8  // waves / SIMD of wf_trace_kernel (64 VGPRs; its spills are refill-time constants)
+#endif
+template <int STACK, int BLK, int NCAP>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))) void wf_trace_kernel(RenderArgs a, WfArgs w) {
+  constexpr uint32_t FEAT = F_SPHERES;
+  __shared__ uint16_t stk16_all[STACK * BLK];
+  __shared__ float4 nodes_lds[NCAP * 8];
+  __shared__ StartArgs start_lds[1];
+  __shared__ uint32_t pool_lds[BLK / 64][3];
+  for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
+    nodes_lds[k] = reinterpret_cast<const float4*>(a.scene.nodes)[k];
+  if (threadIdx.x == 0) fill_start_args(a, start_lds[0]);
+  const uint32_t par = w.par;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the queues the coming shading appends to (last iteration's inputs)
+    w.cnt[1 - par] = 0u;
+    w.cnt[3 - par] = 0u;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t* const pool = pool_lds[threadIdx.x >> 6];
+  if (lane == 0) { pool[0] = 0u; pool[1] = 0u; }
+  __syncthreads();
+  const StartArgs& SA = start_lds[0];
+  uint16_t* stk16 = stk16_all + threadIdx.x;
+  const DevScene& S = a.scene;
+  const uint32_t nq = w.cnt[par], total = nq + w.cnt[2 + par];
+  const uint64_t P = a.n_paths;
+  uint32_t cnt[15];
+  bool exhausted = false, has = false;
+  TraceState ts;
+  ts.on = false;
+  Ray ray;
+  ray.o = mk(0.f, 0.f, 0.f);
+  ray.d = ray.o;
+  ray.time = 0.f;
+  uint32_t slot = 0;
+  unsigned long long nrays = 0;
+  for (;;) {
+    const uint64_t need = __ballot(!has);
+    if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
+      const uint32_t n_need = (uint32_t)__popcll(need);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      uint32_t pool_next = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[0]);
+      uint32_t pool_end = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[1]);
+      const uint32_t avail = pool_end - pool_next;
+      uint32_t nb = total, ne = total;
+      if (avail < n_need) {
+        if (lane == 0) pool[2] = atomicAdd(&w.cnt[4], a.batch);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[2]);
+        if (b < total) {
+          nb = b;
+          ne = total - b > a.batch ? b + a.batch : total;
+        } else {
+          exhausted = true;
+        }
+      }
+      bool fresh = false;  // this lane takes a free slot: a new path
+      if (!has) {
+        const uint32_t item = rank < avail ? pool_next + rank : nb + (rank - avail);
+        if (rank < avail || item < ne) {
+          if (item < nq) {
+            slot = w.rayq[par][item];
+            const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot];
+            ray.o = mk(o4.x, o4.y, o4.z);
+            ray.d = mk(d4.x, d4.y, d4.z);
+            ray.time = o4.w;
+            has = true;
+          } else {
+            slot = w.freeq[par][item - nq];
+            fresh = true;
+          }
+        }
+      }
+      const uint64_t fm = __ballot(fresh);
+      if (fm != 0) {  // new path ids for the fresh lanes: one atomic per wave on the pass's dispenser
+        if (lane == 0) pool[2] = (uint32_t)atomicAdd(a.queue, (unsigned long long)__popcll(fm));
+        const uint64_t base = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pool[2]);
+        if (fresh) {
+          const uint32_t r2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+          const uint64_t id = base + r2;
+          PathState st;
+          if (id >= P) {
+            w.hit[slot] = make_uint2(0u, (uint32_t)-3);
+          } else if (start_path<true>(SA, id, st)) {
+            ray = st.ray;
+            w.thr[slot] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
+            w.rng[slot] = st.rng;
+            w.pid[slot] = st.pid;
+            w.ray_o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.time);
+            w.ray_d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+            has = true;
+          } else {
+            w.hit[slot] = make_uint2(0u, (uint32_t)-4);
+          }
+        }
+      }
+      if (avail >= n_need) {
+        pool_next += n_need;
+      } else {
+        pool_next = nb + (n_need - avail);
+        pool_end = ne;
+        if (pool_next > pool_end) pool_next = pool_end;
+      }
+      if (lane == 0) { pool[0] = pool_next; pool[1] = pool_end; }
+    }
+    if (__ballot(has) == 0) {
+      if (exhausted) break;
+      continue;
+    }
+    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
+    if (!has) continue;
+    if (!ts.on) trace_begin<false, FEAT>(S, ray, ts, cnt, 0);
+    const uint32_t act = (uint32_t)__popcll(__ballot(1));
+    const uint32_t quota = (act * a.quota16 + 15u) >> 4;
+    const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
+    trace_run<false, STACK, false, FEAT, BLK, NCAP, false>(S, ray, ts, nullptr, nullptr, 0u, cnt, quota, leaf_thr, 0,
+                                                          a.err, nullptr, nodes_lds, stk16);
+    if (ts.node >= 0 || ts.sp > 0) continue;  // suspended: resume next round
+    ts.on = false;
+    w.hit[slot] = make_uint2(__float_as_uint(ts.b.t), (uint32_t)ts.b.prim);
+    has = false;
+  }
+  if (lane == 0 && nrays) atomicAdd(a.counters, nrays);
+}
+
+// appends this lane's slot to q (count c) if `on`: one atomic per wave
+__device__ __forceinline__ void wf_append(bool on, uint32_t* q, uint32_t* c, uint32_t slot) {
+  const uint64_t m = __ballot(on);
+  if (m == 0) return;
+  const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
+  uint32_t base = 0;
+  if ((uint32_t)__lane_id() == first) base = atomicAdd(c, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, (int)first, 64);
+  if (on) q[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
+}
+
+__global__ __launch_bounds__(256) void wf_shade_kernel(RenderArgs a, WfArgs w) {
+  constexpr uint32_t FEAT = F_SPHERES;
+  const uint32_t par = w.par, nq = w.cnt[par], total = nq + w.cnt[2 + par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.cnt[4] = 0u;  // the next trace's item head (this trace is done)
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  bool to_ray = false, to_free = false;
+  uint32_t slot = 0;
+  if (i < total) {
+    slot = i < nq ? w.rayq[par][i] : w.freeq[par][i - nq];
+    const uint2 hv = w.hit[slot];
+    const int32_t prim = (int32_t)hv.y;
+    if (prim == -4) {
+      to_free = true;
+    } else if (prim != -3) {
+      const DevScene& S = a.scene;
+      const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot], T4 = w.thr[slot];
+      Ray r;
+      r.o = mk(o4.x, o4.y, o4.z);
+      r.d = mk(d4.x, d4.y, d4.z);
+      r.time = o4.w;
+      const V3 T = mk(T4.x, T4.y, T4.z);
+      uint32_t depth = __float_as_uint(T4.w);
+      uint64_t rng = w.rng[slot];
+      const Best b{__uint_as_float(hv.x), 0u, prim, 0.0f, 0.0f};
+      bool done = false;
+      V3 L = mk(0.f, 0.f, 0.f);
+      if (b.prim < 0) {  // lib.rs:102-105 (a tripped guard, prim -2, shades as a miss; the error is reported)
+        L = mul(T, ld3(a.bg));
+        done = true;
+      } else {
+        const DevShade sh = S.shade[b.prim];
+        const Rec h = hit_record<FEAT>(S, r, b, sh.kind);
+        const uint32_t mt = sh.kind & 0xffu, mode = (sh.kind >> 8) & 0xfu;
+        const bool light = mt == MT_LIGHT, lam = mt == MT_LAMBERT, met = mt == MT_METAL;
+        V3 rs = mk(0.f, 0.f, 0.f);
+        if (lam || met) rs = rand_in_unit_sphere<true>(rng);  // vec3.rs:101-108
+        const V3 ud = unit(lam ? rs : r.d);
+        V3 att = mk(1.f, 1.f, 1.f);
+        if (met) {
+          att = ld3(sh.a);
+        } else if (light || lam) {
+          if (mode == SM_SOLID) att = ld3(sh.a);
+          else if (mode == SM_CHECKER)
+            att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a) : ld3(sh.b);
+        }
+        if (light) {
+          L = mul(T, att);
+          done = true;
+        } else {
+          V3 dir = rs;
+          if (lam) {  // material.rs:42-56
+            dir = add(h.n, ud);
+            if (near_zero(dir)) dir = h.n;
+          } else if (met) {  // material.rs:78-95
+            dir = add(reflect(ud, h.n), scale(rs, sh.param));
+            done = !(dot(dir, h.n) > 0.0f);
+          } else {  // Dielectric, material.rs:116-142
+            const float ratio = h.front ? sh.a[0] : sh.param;
+            const float r0 = h.front ? sh.a[1] : sh.a[2];
+            const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
+            const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+            const bool cannot = (ratio * sin_t) > 1.0f;
+            if (cannot || reflectance(cos_t, r0) > gen_f32(rng)) dir = reflect(ud, h.n);
+            else dir = refract(ud, h.n, ratio);
+          }
+          const V3 T2 = mul(T, att);
+          if (!done) done = --depth == 0u;  // lib.rs:98-100
+          if (!done) {
+            w.ray_o[slot] = make_float4(h.p.x, h.p.y, h.p.z, r.time);
+            w.ray_d[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
+            w.thr[slot] = make_float4(T2.x, T2.y, T2.z, __uint_as_float(depth));
+            w.rng[slot] = rng;
+          }
+        }
+      }
+      if (done) {
+        float* o = a.sbuf + (size_t)w.pid[slot] * 3u;
+        __builtin_nontemporal_store(L.x, o);
+        __builtin_nontemporal_store(L.y, o + 1);
+        __builtin_nontemporal_store(L.z, o + 2);
+        to_free = true;
+      } else {
+        to_ray = true;
+      }
+    }
+  }
+  wf_append(to_ray, w.rayq[1 - par], &w.cnt[1 - par], slot);
+  wf_append(to_free, w.freeq[1 - par], &w.cnt[3 - par], slot);
+}
+
+__global__ void wf_init_kernel(WfArgs w) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < w.n_slots) w.freeq[0][i] = i;
+  if (i == 0) {
+    w.cnt[0] = 0u; w.cnt[1] = 0u; w.cnt[2] = w.n_slots; w.cnt[3] = 0u; w.cnt[4] = 0u;
+  }
+}
+
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
                                     uint32_t n_tiles, const float* packed, float* img) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1786,6 +2046,10 @@ void release(Scene& s) {
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
     for (void* e : c.gev)
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
+    for (void* e : c.wf_ev)
+      if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
+    if (c.wf_block) hipFree(c.wf_block);
+    if (c.wf_host) hipHostFree(c.wf_host);
     if (c.stream) hipStreamDestroy(static_cast<hipStream_t>(c.stream));
     for (auto& e : c.kev)
       for (void* x : e)
@@ -1992,6 +2256,75 @@ int check_guard(DeviceCopy& c) {
   return RTW_OK;
 }
 
+// The wavefront prototype's iterations for one pass (dev::WfArgs): trace + shade launches in chunks of 16
+// iterations; after each chunk the next iteration's ray-queue count and the path dispenser are copied to
+// pinned memory, and the chunk before it is checked (so the GPU always has a chunk queued): the pass is done
+// once no ray is queued and every path id has been handed out.
+static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
+  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21)));
+  const size_t need = (size_t)N * (16 * 3 + 8 + 4 + 8 + 16) + 256;
+  if (need > c.wf_bytes) {
+    if (c.wf_block) HIPCHK(hipFree(c.wf_block), "hipFree(wavefront)");
+    c.wf_block = nullptr;
+    c.wf_bytes = 0;
+    HIPCHK(hipMalloc(&c.wf_block, need), "hipMalloc(wavefront)");
+    c.wf_bytes = need;
+  }
+  if (!c.wf_host) HIPCHK(hipHostMalloc((void**)&c.wf_host, 64, hipHostMallocDefault), "hipHostMalloc(wavefront)");
+  for (void*& e : c.wf_ev)
+    if (!e) {
+      hipEvent_t x;
+      HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming), "hipEventCreate");
+      e = x;
+    }
+  uint8_t* p = static_cast<uint8_t*>(c.wf_block);
+  dev::WfArgs wa;
+  wa.ray_o = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
+  wa.ray_d = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
+  wa.thr = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
+  wa.rng = reinterpret_cast<uint64_t*>(p); p += (size_t)N * 8;
+  wa.hit = reinterpret_cast<uint2*>(p); p += (size_t)N * 8;
+  wa.pid = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4;
+  for (int k = 0; k < 2; ++k) { wa.rayq[k] = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4; }
+  for (int k = 0; k < 2; ++k) { wa.freeq[k] = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4; }
+  wa.cnt = reinterpret_cast<uint32_t*>(p);
+  wa.n_slots = N;
+  wa.par = 0;
+  hipLaunchKernelGGL(dev::wf_init_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, wa);
+  HIPCHK(hipGetLastError(), "wf_init_kernel");
+  constexpr int STACK = 16, BLK = 1024, NCAP = 144;
+  auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
+  const dim3 tgrid(per_cu * cus), sgrid((N + 255) / 256);
+  const uint32_t chunk = (uint32_t)std::max(1, env_int("RTW_WF_CHUNK", 16));
+  const uint64_t P = a.n_paths;
+  // items a trace wave takes per atomic: an iteration holds only ~N / resident waves items per wave (256 at
+  // 2 M slots), so the megakernel's 1024-id batches would leave most waves idle
+  a.batch = (uint32_t)std::min(4096, std::max(64, env_int("RTW_WF_BATCH", 64)));
+  for (uint32_t ch = 0;; ++ch) {
+    for (uint32_t k = 0; k < chunk; ++k) {
+      hipLaunchKernelGGL(trace, tgrid, dim3(BLK), 0, stream, a, wa);
+      hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(256), 0, stream, a, wa);
+      wa.par ^= 1u;
+    }
+    HIPCHK(hipGetLastError(), "wavefront launches");
+    uint32_t* hb = c.wf_host + 4 * (ch & 1u);
+    HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par, 4, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
+    HIPCHK(hipMemcpyAsync(hb + 2, a.queue, 8, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
+    HIPCHK(hipEventRecord(static_cast<hipEvent_t>(c.wf_ev[ch & 1u]), stream), "hipEventRecord");
+    if (ch >= 1) {
+      HIPCHK(hipEventSynchronize(static_cast<hipEvent_t>(c.wf_ev[(ch - 1) & 1u])), "wavefront progress");
+      const uint32_t* pb = c.wf_host + 4 * ((ch - 1) & 1u);
+      const uint64_t taken = (uint64_t)pb[2] | ((uint64_t)pb[3] << 32);
+      if (pb[0] == 0u && taken >= P) break;
+    }
+    if (ch > (1u << 22)) return fail(RTW_EINVAL, "wavefront: no progress");
+  }
+  return RTW_OK;
+}
+
 int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float bg[3], uint32_t w, uint32_t h,
                    uint32_t spp, uint32_t max_depth, uint64_t seed, const TileSet& ts, float* d_out, void* stream_,
                    uint32_t flags, void* ev0_, void* ev1_) {
@@ -2101,6 +2434,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       c.spill_bytes = spill_bytes;
     }
     a.spill = c.spill;
+    // the wavefront prototype (knob RTW_WAVEFRONT=1): the 1024-lane LDS-node sphere worlds, plain renders only
+    const bool wavefront = env_int("RTW_WAVEFRONT", 0) == 1 && !count && var.k16 && var.block == 1024u;
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
@@ -2110,8 +2445,12 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
       HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
-      hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
-      HIPCHK(hipGetLastError(), "path_kernel launch");
+      if (wavefront) {
+        if (int e = run_wavefront(c, a, stream)) return e;
+      } else {
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
+        HIPCHK(hipGetLastError(), "path_kernel launch");
+      }
       HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
       c.kev_head = (c.kev_head + 1) % 64u;
       c.kev_count = std::min(c.kev_count + 1u, 64u);

@@ -109,6 +109,11 @@ struct DeviceCopy {
   void* ev[2] = {nullptr, nullptr};        // hipEvent_t pair timing rtw_render / multi calls
   void* stream = nullptr;                  // hipStream_t of rtw_render_multi on this device
   void* gev[2] = {nullptr, nullptr};       // hipEvent_t pair around rtw_render_multi's gather (device 0)
+  // wavefront prototype (RTW_WAVEFRONT=1): slot state + queues, the host-visible progress words, their events
+  void* wf_block = nullptr;
+  size_t wf_bytes = 0;
+  uint32_t* wf_host = nullptr;             // pinned: per in-flight chunk, (rayq count, path ids taken lo, hi)
+  void* wf_ev[2] = {nullptr, nullptr};
 };
 
 struct Scene {

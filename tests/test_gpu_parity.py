@@ -133,6 +133,20 @@ def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
         assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
 
 
+@pytest.mark.parametrize("slots", ["", "4096", "65536"])
+def test_wavefront_prototype_bit_exact(gpu, orc, monkeypatch, slots):
+    """RTW_WAVEFRONT=1: the trace / shade split across kernels with the slot state and
+    the ray / free-slot queues in global memory renders the same image and ray count as the oracle; small
+    slot counts (RTW_WF_SLOTS) force many iterations, slot reuse and the end-of-frame drain."""
+    monkeypatch.setenv("RTW_WAVEFRONT", "1")
+    if slots:
+        monkeypatch.setenv("RTW_WF_SLOTS", slots)
+    name, aspect, w, h, spp = SCENES[0]
+    g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
+    assert st["rays"] == rays
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
+
+
 def test_pass_with_path_ids_above_2_31(gpu, monkeypatch):
     """One pass of more than 2^31 paths (monument-4k's passes hold 2^32): path ids past 2^31 must
     dispense and index correctly.  The same frame split into 2^30-path passes is the reference."""
