@@ -1640,15 +1640,20 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
 
 // ---- wavefront prototype (knob RTW_WAVEFRONT=1): the megakernel's loop split across
 // kernels by phase, so that every wave of a phase works on rays of that phase only.  Each iteration:
-//   wf_trace_kernel (persistent, LDS node table): its waves take items from this iteration's queues -- slots
-//     holding a scattered ray (rayq), then free slots (freeq), which start a new path (start_path, the path id
-//     from the same global dispenser as the megakernel) -- and trace them with the same resumable walk; a
-//     lane whose query is done stores (t, prim) and is refilled at once (no shading phase to wait for).
-//   wf_shade_kernel (one thread per item): the megakernel's shading body for the slot's hit; a finished path
-//     writes its sample and returns its slot to the next freeq, a scattered ray goes to the next rayq
-//     (wave-aggregated appends: one atomic per wave and queue).
-// Slot state lives in global memory (SoA, ~80 B per slot; RTW_WF_SLOTS slots, sized for the 256 MB
-// Infinity Cache).  Pixels depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
+//   wf_trace_kernel (persistent, LDS node table): wave gw of W takes items gw, gw + W, gw + 2W, ... of this
+//     iteration's queues -- slots holding a scattered ray (rayq), then free slots (freeq), which start a new
+//     path (start_path; path ids from a per-wave pool refilled 1024 at a time from the pass's dispenser, the
+//     pool kept across launches) -- and traces them with the megakernel's resumable walk; a lane whose query
+//     is done stores (t, prim) and is refilled at once: no shading phase to wait for.
+//   wf_shade_kernel (one thread per item, 1024-thread blocks): the megakernel's shading body for the slot's
+//     hit; a finished path writes its sample and returns its slot to the next freeq, a scattered ray goes to
+//     the next rayq.  Appends are counted in LDS: one global atomic per block and queue, into one of 8 queue
+//     shards (block index mod 8), so no address sees more than ~N / 8192 atomics per iteration.
+// (The first version dispensed items and appended with one atomic per wave on one address each: ~100 K
+// same-address atomics per iteration at ~13 ns each made it 15x slower than the megakernel, r04b / r04c.)
+// Slot state lives in global memory (SoA, ~100 B per slot with the queues; RTW_WF_SLOTS slots).  Pixels
+// depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
+constexpr uint32_t WF_SHARDS = 8;
 struct WfArgs {
   float4* ray_o;       // o.xyz, time
   float4* ray_d;       // d.xyz, -
@@ -1656,12 +1661,32 @@ struct WfArgs {
   uint64_t* rng;       // the path's xoroshiro64* state
   uint32_t* pid;       // path id within the pass
   uint2* hit;          // (t bits, prim); prim -3: no path left for the slot, -4: its id was off the image
-  uint32_t* rayq[2];   // slots with a ray to trace (iteration parity p reads [p], shading appends to [1 - p])
-  uint32_t* freeq[2];  // slots to start a new path in
-  uint32_t* cnt;       // [0, 1] rayq counts, [2, 3] freeq counts, [4] trace item head
-  uint32_t n_slots;
+  uint32_t* rayq[2];   // [shard][shard_cap] slots with a ray to trace (parity p reads [p], shading appends to [1 - p])
+  uint32_t* freeq[2];  // [shard][shard_cap] slots to start a new path in
+  uint32_t* cnt;       // [p * 8 + s] rayq counts, [16 + p * 8 + s] freeq counts, [32..33] path ids consumed (u64)
+  uint2* wpool;        // per trace wave: its path-id pool [next, end), kept across launches
+  uint32_t n_slots, shard_cap;
   uint32_t par;
 };
+
+// this iteration's item k -> its slot: items are the 8 rayq shards, then the 8 freeq shards, in order;
+// pre[0..16] are their prefix counts
+__device__ __forceinline__ uint32_t wf_slot(const WfArgs& w, const uint32_t* pre, uint32_t k, bool& fresh) {
+  uint32_t q = 0;
+#pragma unroll
+  for (int s = 1; s < 16; ++s) q += k >= pre[s] ? 1u : 0u;
+  fresh = q >= WF_SHARDS;
+  const uint32_t* Q = fresh ? w.freeq[w.par] : w.rayq[w.par];
+  return Q[(size_t)(q & (WF_SHARDS - 1)) * w.shard_cap + (k - pre[q])];
+}
+__device__ __forceinline__ void wf_prefix(const WfArgs& w, uint32_t* pre) {  // thread 0 of the block
+  uint32_t t = 0;
+  for (int s = 0; s < 16; ++s) {
+    pre[s] = t;
+    t += w.cnt[s < 8 ? w.par * 8 + s : 16 + w.par * 8 + (s - 8)];
+  }
+  pre[16] = t;
+}
 
 #ifndef WF_OCC
 #define WF_OCC 8  // waves / SIMD of wf_trace_kernel (64 VGPRs; its spills are refill-time constants)
@@ -1672,23 +1697,33 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
   __shared__ uint16_t stk16_all[STACK * BLK];
   __shared__ float4 nodes_lds[NCAP * 8];
   __shared__ StartArgs start_lds[1];
-  __shared__ uint32_t pool_lds[BLK / 64][3];
+  __shared__ uint32_t pre[17];
+  __shared__ uint32_t wstate[BLK / 64][4];  // per wave: item position, pool next, pool end, scratch
+  __shared__ unsigned long long consumed;
   for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
     nodes_lds[k] = reinterpret_cast<const float4*>(a.scene.nodes)[k];
-  if (threadIdx.x == 0) fill_start_args(a, start_lds[0]);
-  const uint32_t par = w.par;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the queues the coming shading appends to (last iteration's inputs)
-    w.cnt[1 - par] = 0u;
-    w.cnt[3 - par] = 0u;
+  const uint32_t par = w.par, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t gw = blockIdx.x * (BLK / 64) + wv, W = gridDim.x * (BLK / 64);
+  if (threadIdx.x == 0) {
+    fill_start_args(a, start_lds[0]);
+    wf_prefix(w, pre);
+    consumed = 0;
   }
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t* const pool = pool_lds[threadIdx.x >> 6];
-  if (lane == 0) { pool[0] = 0u; pool[1] = 0u; }
+  if (blockIdx.x == 0 && threadIdx.x < 16) {  // the queues the coming shading appends to (last iteration's inputs)
+    w.cnt[(1 - par) * 8 + threadIdx.x % 8 + (threadIdx.x < 8 ? 0 : 16)] = 0u;
+  }
+  uint32_t* const ws = wstate[wv];
+  if (lane == 0) {
+    const uint2 pl = w.wpool[gw];
+    ws[0] = 0u;
+    ws[1] = pl.x;
+    ws[2] = pl.y;
+  }
   __syncthreads();
   const StartArgs& SA = start_lds[0];
   uint16_t* stk16 = stk16_all + threadIdx.x;
   const DevScene& S = a.scene;
-  const uint32_t nq = w.cnt[par], total = nq + w.cnt[2 + par];
+  const uint32_t total = pre[16];
   const uint64_t P = a.n_paths;
   uint32_t cnt[15];
   bool exhausted = false, has = false;
@@ -1698,7 +1733,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
   ray.o = mk(0.f, 0.f, 0.f);
   ray.d = ray.o;
   ray.time = 0.f;
-  uint32_t slot = 0;
+  uint32_t slot = 0, n_consumed = 0;
   unsigned long long nrays = 0;
   for (;;) {
     const uint64_t need = __ballot(!has);
@@ -1706,46 +1741,40 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
       const uint32_t n_need = (uint32_t)__popcll(need);
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      uint32_t pool_next = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[0]);
-      uint32_t pool_end = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[1]);
-      const uint32_t avail = pool_end - pool_next;
-      uint32_t nb = total, ne = total;
-      if (avail < n_need) {
-        if (lane == 0) pool[2] = atomicAdd(&w.cnt[4], a.batch);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[2]);
-        if (b < total) {
-          nb = b;
-          ne = total - b > a.batch ? b + a.batch : total;
-        } else {
-          exhausted = true;
-        }
-      }
-      bool fresh = false;  // this lane takes a free slot: a new path
+      const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[0]);
+      bool fresh = false;
       if (!has) {
-        const uint32_t item = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if (rank < avail || item < ne) {
-          if (item < nq) {
-            slot = w.rayq[par][item];
+        const uint64_t item = (uint64_t)gw + (uint64_t)W * (pos + rank);
+        if (item < total) {
+          slot = wf_slot(w, pre, (uint32_t)item, fresh);
+          if (!fresh) {
             const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot];
             ray.o = mk(o4.x, o4.y, o4.z);
             ray.d = mk(d4.x, d4.y, d4.z);
             ray.time = o4.w;
             has = true;
-          } else {
-            slot = w.freeq[par][item - nq];
-            fresh = true;
           }
         }
       }
+      if ((uint64_t)gw + (uint64_t)W * (pos + n_need) >= total) exhausted = true;
+      if (lane == 0) ws[0] = pos + n_need;
       const uint64_t fm = __ballot(fresh);
-      if (fm != 0) {  // new path ids for the fresh lanes: one atomic per wave on the pass's dispenser
-        if (lane == 0) pool[2] = (uint32_t)atomicAdd(a.queue, (unsigned long long)__popcll(fm));
-        const uint64_t base = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pool[2]);
+      if (fm != 0) {  // new path ids for the fresh lanes, from the wave's pool (one atomic per 1024 ids)
+        const uint32_t nf = (uint32_t)__popcll(fm);
+        const uint32_t pn = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[1]);
+        const uint32_t pe = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[2]);
+        const uint32_t avail = pe - pn;
+        uint64_t nb = P;
+        if (avail < nf) {
+          if (lane == 0) ws[3] = (uint32_t)min((unsigned long long)P, atomicAdd(a.queue, 1024ull));
+          nb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)ws[3]);
+        }
+        const uint64_t ne = nb + 1024u < P ? nb + 1024u : P;
         if (fresh) {
           const uint32_t r2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-          const uint64_t id = base + r2;
+          const uint64_t id = r2 < avail ? (uint64_t)pn + r2 : nb + (r2 - avail);
           PathState st;
-          if (id >= P) {
+          if (id >= (r2 < avail ? (uint64_t)pe : ne)) {
             w.hit[slot] = make_uint2(0u, (uint32_t)-3);
           } else if (start_path<true>(SA, id, st)) {
             ray = st.ray;
@@ -1755,19 +1784,22 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
             w.ray_o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.time);
             w.ray_d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
             has = true;
+            ++n_consumed;
           } else {
             w.hit[slot] = make_uint2(0u, (uint32_t)-4);
+            ++n_consumed;
+          }
+        }
+        if (lane == 0) {
+          if (avail >= nf) {
+            ws[1] = pn + nf;
+          } else {
+            const uint64_t nn = nb + (nf - avail);
+            ws[1] = (uint32_t)(nn < ne ? nn : ne);
+            ws[2] = (uint32_t)ne;
           }
         }
       }
-      if (avail >= n_need) {
-        pool_next += n_need;
-      } else {
-        pool_next = nb + (n_need - avail);
-        pool_end = ne;
-        if (pool_next > pool_end) pool_next = pool_end;
-      }
-      if (lane == 0) { pool[0] = pool_next; pool[1] = pool_end; }
     }
     if (__ballot(has) == 0) {
       if (exhausted) break;
@@ -1787,28 +1819,36 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
     has = false;
   }
   if (lane == 0 && nrays) atomicAdd(a.counters, nrays);
+  // path ids consumed (started or off the image): summed per workgroup, one atomic per workgroup
+  unsigned long long c = n_consumed;
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if (lane == 0) {
+    if (c) atomicAdd(&consumed, c);
+    w.wpool[gw] = make_uint2(ws[1], ws[2]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && consumed) atomicAdd(reinterpret_cast<unsigned long long*>(w.cnt + 32), consumed);
 }
 
-// appends this lane's slot to q (count c) if `on`: one atomic per wave
-__device__ __forceinline__ void wf_append(bool on, uint32_t* q, uint32_t* c, uint32_t slot) {
-  const uint64_t m = __ballot(on);
-  if (m == 0) return;
-  const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
-  uint32_t base = 0;
-  if ((uint32_t)__lane_id() == first) base = atomicAdd(c, (uint32_t)__popcll(m));
-  base = (uint32_t)__shfl((int)base, (int)first, 64);
-  if (on) q[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
-}
-
-__global__ __launch_bounds__(256) void wf_shade_kernel(RenderArgs a, WfArgs w) {
+__global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) {
   constexpr uint32_t FEAT = F_SPHERES;
-  const uint32_t par = w.par, nq = w.cnt[par], total = nq + w.cnt[2 + par];
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.cnt[4] = 0u;  // the next trace's item head (this trace is done)
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  __shared__ uint32_t pre[17];
+  __shared__ uint32_t nap[2], base[2];
+  const uint32_t par = w.par;
+  if (threadIdx.x == 0) {
+    wf_prefix(w, pre);
+    nap[0] = 0u;
+    nap[1] = 0u;
+  }
+  __syncthreads();
+  const uint32_t total = pre[16];
+  if (blockIdx.x * 1024u >= total) return;  // whole block idle (uniform)
+  const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
   bool to_ray = false, to_free = false;
   uint32_t slot = 0;
   if (i < total) {
-    slot = i < nq ? w.rayq[par][i] : w.freeq[par][i - nq];
+    bool fresh_item;
+    slot = wf_slot(w, pre, i, fresh_item);
     const uint2 hv = w.hit[slot];
     const int32_t prim = (int32_t)hv.y;
     if (prim == -4) {
@@ -1886,16 +1926,24 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderArgs a, WfArgs w) {
       }
     }
   }
-  wf_append(to_ray, w.rayq[1 - par], &w.cnt[1 - par], slot);
-  wf_append(to_free, w.freeq[1 - par], &w.cnt[3 - par], slot);
+  // appends: offsets from LDS counters, then one global atomic per queue for the block's shard
+  const uint32_t oray = to_ray ? atomicAdd(&nap[0], 1u) : 0u, ofree = to_free ? atomicAdd(&nap[1], 1u) : 0u;
+  __syncthreads();
+  const uint32_t sh = blockIdx.x & (WF_SHARDS - 1);
+  if (threadIdx.x == 0) {
+    base[0] = nap[0] ? atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap[0]) : 0u;
+    base[1] = nap[1] ? atomicAdd(&w.cnt[16 + (1 - par) * 8 + sh], nap[1]) : 0u;
+  }
+  __syncthreads();
+  if (to_ray) w.rayq[1 - par][(size_t)sh * w.shard_cap + base[0] + oray] = slot;
+  if (to_free) w.freeq[1 - par][(size_t)sh * w.shard_cap + base[1] + ofree] = slot;
 }
 
-__global__ void wf_init_kernel(WfArgs w) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < w.n_slots) w.freeq[0][i] = i;
-  if (i == 0) {
-    w.cnt[0] = 0u; w.cnt[1] = 0u; w.cnt[2] = w.n_slots; w.cnt[3] = 0u; w.cnt[4] = 0u;
-  }
+__global__ void wf_init_kernel(WfArgs w, uint32_t n_waves) {  // n_slots is a multiple of 8
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, per = w.n_slots / WF_SHARDS;
+  if (i < w.n_slots) w.freeq[0][(size_t)(i / per) * w.shard_cap + i % per] = i;  // shard s: slots [s per, (s + 1) per)
+  if (i < n_waves) w.wpool[i] = make_uint2(0u, 0u);
+  if (i < 34) w.cnt[i] = (i >= 16 && i < 24) ? per : 0u;
 }
 
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
@@ -2261,8 +2309,16 @@ int check_guard(DeviceCopy& c) {
 // pinned memory, and the chunk before it is checked (so the GPU always has a chunk queued): the pass is done
 // once no ray is queued and every path id has been handed out.
 static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
-  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21)));
-  const size_t need = (size_t)N * (16 * 3 + 8 + 4 + 8 + 16) + 256;
+  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21))) & ~7u;
+  const uint32_t cap = N / dev::WF_SHARDS + 1024u;  // a shard gets <= ceil(blocks / 8) blocks of 1024 items
+  constexpr int STACK = 16, BLK = 1024, NCAP = 144;
+  auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
+  const uint32_t tblocks = (uint32_t)(per_cu * cus), n_waves = tblocks * (BLK / 64);
+  const size_t qbytes = (size_t)dev::WF_SHARDS * cap * 4;
+  const size_t need = (size_t)N * (16 * 3 + 8 + 8 + 4) + 4 * qbytes + (size_t)n_waves * 8 + 256;
   if (need > c.wf_bytes) {
     if (c.wf_block) HIPCHK(hipFree(c.wf_block), "hipFree(wavefront)");
     c.wf_block = nullptr;
@@ -2270,7 +2326,7 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
     HIPCHK(hipMalloc(&c.wf_block, need), "hipMalloc(wavefront)");
     c.wf_bytes = need;
   }
-  if (!c.wf_host) HIPCHK(hipHostMalloc((void**)&c.wf_host, 64, hipHostMallocDefault), "hipHostMalloc(wavefront)");
+  if (!c.wf_host) HIPCHK(hipHostMalloc((void**)&c.wf_host, 256, hipHostMallocDefault), "hipHostMalloc(wavefront)");
   for (void*& e : c.wf_ev)
     if (!e) {
       hipEvent_t x;
@@ -2285,40 +2341,37 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
   wa.rng = reinterpret_cast<uint64_t*>(p); p += (size_t)N * 8;
   wa.hit = reinterpret_cast<uint2*>(p); p += (size_t)N * 8;
   wa.pid = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4;
-  for (int k = 0; k < 2; ++k) { wa.rayq[k] = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4; }
-  for (int k = 0; k < 2; ++k) { wa.freeq[k] = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4; }
+  for (int k = 0; k < 2; ++k) { wa.rayq[k] = reinterpret_cast<uint32_t*>(p); p += qbytes; }
+  for (int k = 0; k < 2; ++k) { wa.freeq[k] = reinterpret_cast<uint32_t*>(p); p += qbytes; }
+  wa.wpool = reinterpret_cast<uint2*>(p); p += (size_t)n_waves * 8;
   wa.cnt = reinterpret_cast<uint32_t*>(p);
   wa.n_slots = N;
+  wa.shard_cap = cap;
   wa.par = 0;
-  hipLaunchKernelGGL(dev::wf_init_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, wa);
+  const uint32_t ninit = std::max(N, n_waves);
+  hipLaunchKernelGGL(dev::wf_init_kernel, dim3((ninit + 255) / 256), dim3(256), 0, stream, wa, n_waves);
   HIPCHK(hipGetLastError(), "wf_init_kernel");
-  constexpr int STACK = 16, BLK = 1024, NCAP = 144;
-  auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
-  const dim3 tgrid(per_cu * cus), sgrid((N + 255) / 256);
+  const dim3 tgrid(tblocks), sgrid((N + 1023) / 1024);
   const uint32_t chunk = (uint32_t)std::max(1, env_int("RTW_WF_CHUNK", 16));
   const uint64_t P = a.n_paths;
-  // items a trace wave takes per atomic: an iteration holds only ~N / resident waves items per wave (256 at
-  // 2 M slots), so the megakernel's 1024-id batches would leave most waves idle
-  a.batch = (uint32_t)std::min(4096, std::max(64, env_int("RTW_WF_BATCH", 64)));
   for (uint32_t ch = 0;; ++ch) {
     for (uint32_t k = 0; k < chunk; ++k) {
       hipLaunchKernelGGL(trace, tgrid, dim3(BLK), 0, stream, a, wa);
-      hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(256), 0, stream, a, wa);
+      hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(1024), 0, stream, a, wa);
       wa.par ^= 1u;
     }
     HIPCHK(hipGetLastError(), "wavefront launches");
-    uint32_t* hb = c.wf_host + 4 * (ch & 1u);
-    HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par, 4, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
-    HIPCHK(hipMemcpyAsync(hb + 2, a.queue, 8, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
+    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // [0..7] next rayq shard counts, [8..9] ids consumed
+    HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par * 8, 32, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
+    HIPCHK(hipMemcpyAsync(hb + 8, wa.cnt + 32, 8, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
     HIPCHK(hipEventRecord(static_cast<hipEvent_t>(c.wf_ev[ch & 1u]), stream), "hipEventRecord");
     if (ch >= 1) {
       HIPCHK(hipEventSynchronize(static_cast<hipEvent_t>(c.wf_ev[(ch - 1) & 1u])), "wavefront progress");
-      const uint32_t* pb = c.wf_host + 4 * ((ch - 1) & 1u);
-      const uint64_t taken = (uint64_t)pb[2] | ((uint64_t)pb[3] << 32);
-      if (pb[0] == 0u && taken >= P) break;
+      const uint32_t* pb = c.wf_host + 32 * ((ch - 1) & 1u);
+      uint64_t rays = 0;
+      for (int s = 0; s < 8; ++s) rays += pb[s];
+      const uint64_t consumed = (uint64_t)pb[8] | ((uint64_t)pb[9] << 32);
+      if (rays == 0 && consumed >= P) break;  // every path id started (or off the image) and no ray left
     }
     if (ch > (1u << 22)) return fail(RTW_EINVAL, "wavefront: no progress");
   }
