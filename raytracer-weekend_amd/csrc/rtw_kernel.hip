@@ -1641,17 +1641,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
 // ---- wavefront prototype (knob RTW_WAVEFRONT=1): the megakernel's loop split across
 // kernels by phase, so that every wave of a phase works on rays of that phase only.  Each iteration:
 //   wf_trace_kernel (persistent, LDS node table): wave gw of W takes items gw, gw + W, gw + 2W, ... of this
-//     iteration's queues -- slots holding a scattered ray (rayq), then free slots (freeq), which start a new
-//     path (start_path; path ids from a per-wave pool refilled 1024 at a time from the pass's dispenser, the
-//     pool kept across launches) -- and traces them with the megakernel's resumable walk; a lane whose query
-//     is done stores (t, prim) and is refilled at once: no shading phase to wait for.
+//     iteration's ray queue (no atomics), traces them with the megakernel's resumable walk, and stores
+//     (t, prim) per slot; a lane whose query is done is refilled at once (no shading phase to wait for).
 //   wf_shade_kernel (one thread per item, 1024-thread blocks): the megakernel's shading body for the slot's
-//     hit; a finished path writes its sample and returns its slot to the next freeq, a scattered ray goes to
-//     the next rayq.  Appends are counted in LDS: one global atomic per block and queue, into one of 8 queue
-//     shards (block index mod 8), so no address sees more than ~N / 8192 atomics per iteration.
+//     hit; a scattered ray goes to the next ray queue; a finished path writes its sample, and the block's
+//     finished slots, compacted in LDS, start new paths with full lanes (start_path; path ids 8 k + shard
+//     from one of 8 dispensers, one atomic per block) and join the next ray queue too.
+//   Queue appends are counted in LDS: one global atomic per block, into one of 8 queue shards (block index
+//   mod 8).  The frame is done when an iteration leaves the ray queue empty (every slot out of path ids).
 // (The first version dispensed items and appended with one atomic per wave on one address each: ~100 K
 // same-address atomics per iteration at ~13 ns each made it 15x slower than the megakernel, r04b / r04c.)
-// Slot state lives in global memory (SoA, ~100 B per slot with the queues; RTW_WF_SLOTS slots).  Pixels
+// Slot state lives in global memory (SoA, ~80 B per slot with the queues; RTW_WF_SLOTS slots).  Pixels
 // depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
 constexpr uint32_t WF_SHARDS = 8;
 struct WfArgs {
@@ -1660,80 +1660,59 @@ struct WfArgs {
   float4* thr;         // T.xyz, remaining depth (bits)
   uint64_t* rng;       // the path's xoroshiro64* state
   uint32_t* pid;       // path id within the pass
-  uint2* hit;          // (t bits, prim); prim -3: no path left for the slot, -4: its id was off the image
+  uint2* hit;          // (t bits, prim)
   uint32_t* rayq[2];   // [shard][shard_cap] slots with a ray to trace (parity p reads [p], shading appends to [1 - p])
-  uint32_t* freeq[2];  // [shard][shard_cap] slots to start a new path in
-  uint32_t* cnt;       // [p * 8 + s] rayq counts, [16 + p * 8 + s] freeq counts, [32..33] path ids consumed (u64)
-  uint2* wpool;        // per trace wave: its path-id pool [next, end), kept across launches
+  uint32_t* cnt;       // [p * 8 + s] ray queue shard counts, [16 + s] path-id dispensers (k of pid = 8 k + s)
   uint32_t n_slots, shard_cap;
   uint32_t par;
+  uint32_t init;       // 1: wf_shade_kernel only starts a path in every slot (items = all slots)
 };
 
-// this iteration's item k -> its slot: items are the 8 rayq shards, then the 8 freeq shards, in order;
-// pre[0..16] are their prefix counts
-__device__ __forceinline__ uint32_t wf_slot(const WfArgs& w, const uint32_t* pre, uint32_t k, bool& fresh) {
+__device__ __forceinline__ uint32_t wf_slot(const WfArgs& w, const uint32_t* pre, uint32_t k) {
   uint32_t q = 0;
 #pragma unroll
-  for (int s = 1; s < 16; ++s) q += k >= pre[s] ? 1u : 0u;
-  fresh = q >= WF_SHARDS;
-  const uint32_t* Q = fresh ? w.freeq[w.par] : w.rayq[w.par];
-  return Q[(size_t)(q & (WF_SHARDS - 1)) * w.shard_cap + (k - pre[q])];
+  for (int s = 1; s < (int)WF_SHARDS; ++s) q += k >= pre[s] ? 1u : 0u;
+  return w.rayq[w.par][(size_t)q * w.shard_cap + (k - pre[q])];
 }
-__device__ __forceinline__ void wf_prefix(const WfArgs& w, uint32_t* pre) {  // thread 0 of the block
+__device__ __forceinline__ void wf_prefix(const WfArgs& w, uint32_t* pre) {  // one thread of the block
   uint32_t t = 0;
-  for (int s = 0; s < 16; ++s) {
+  for (uint32_t s = 0; s < WF_SHARDS; ++s) {
     pre[s] = t;
-    t += w.cnt[s < 8 ? w.par * 8 + s : 16 + w.par * 8 + (s - 8)];
+    t += w.cnt[w.par * 8 + s];
   }
-  pre[16] = t;
+  pre[WF_SHARDS] = t;
 }
 
 #ifndef WF_OCC
-#define WF_OCC 8  // waves / SIMD of wf_trace_kernel (64 VGPRs; its spills are refill-time constants)
+#define WF_OCC 8  // waves / SIMD of wf_trace_kernel
 #endif
 template <int STACK, int BLK, int NCAP>
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))) void wf_trace_kernel(RenderArgs a, WfArgs w) {
   constexpr uint32_t FEAT = F_SPHERES;
   __shared__ uint16_t stk16_all[STACK * BLK];
   __shared__ float4 nodes_lds[NCAP * 8];
-  __shared__ StartArgs start_lds[1];
-  __shared__ uint32_t pre[17];
-  __shared__ uint32_t wstate[BLK / 64][4];  // per wave: item position, pool next, pool end, scratch
-  __shared__ unsigned long long consumed;
+  __shared__ uint32_t pre[WF_SHARDS + 1];
+  __shared__ uint32_t wpos[BLK / 64];
   for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
     nodes_lds[k] = reinterpret_cast<const float4*>(a.scene.nodes)[k];
   const uint32_t par = w.par, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * (BLK / 64) + wv, W = gridDim.x * (BLK / 64);
-  if (threadIdx.x == 0) {
-    fill_start_args(a, start_lds[0]);
-    wf_prefix(w, pre);
-    consumed = 0;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < 16) {  // the queues the coming shading appends to (last iteration's inputs)
-    w.cnt[(1 - par) * 8 + threadIdx.x % 8 + (threadIdx.x < 8 ? 0 : 16)] = 0u;
-  }
-  uint32_t* const ws = wstate[wv];
-  if (lane == 0) {
-    const uint2 pl = w.wpool[gw];
-    ws[0] = 0u;
-    ws[1] = pl.x;
-    ws[2] = pl.y;
-  }
+  if (threadIdx.x == 0) wf_prefix(w, pre);
+  if (blockIdx.x == 0 && threadIdx.x < WF_SHARDS) w.cnt[(1 - par) * 8 + threadIdx.x] = 0u;  // the coming appends
+  if (lane == 0) wpos[wv] = 0u;
   __syncthreads();
-  const StartArgs& SA = start_lds[0];
   uint16_t* stk16 = stk16_all + threadIdx.x;
   const DevScene& S = a.scene;
-  const uint32_t total = pre[16];
-  const uint64_t P = a.n_paths;
+  const uint32_t total = pre[WF_SHARDS];
   uint32_t cnt[15];
-  bool exhausted = false, has = false;
+  bool exhausted = (uint64_t)gw >= total, has = false;
   TraceState ts;
   ts.on = false;
   Ray ray;
   ray.o = mk(0.f, 0.f, 0.f);
   ray.d = ray.o;
   ray.time = 0.f;
-  uint32_t slot = 0, n_consumed = 0;
+  uint32_t slot = 0;
   unsigned long long nrays = 0;
   for (;;) {
     const uint64_t need = __ballot(!has);
@@ -1741,65 +1720,20 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
       const uint32_t n_need = (uint32_t)__popcll(need);
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[0]);
-      bool fresh = false;
+      const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)wpos[wv]);
       if (!has) {
         const uint64_t item = (uint64_t)gw + (uint64_t)W * (pos + rank);
         if (item < total) {
-          slot = wf_slot(w, pre, (uint32_t)item, fresh);
-          if (!fresh) {
-            const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot];
-            ray.o = mk(o4.x, o4.y, o4.z);
-            ray.d = mk(d4.x, d4.y, d4.z);
-            ray.time = o4.w;
-            has = true;
-          }
+          slot = wf_slot(w, pre, (uint32_t)item);
+          const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot];
+          ray.o = mk(o4.x, o4.y, o4.z);
+          ray.d = mk(d4.x, d4.y, d4.z);
+          ray.time = o4.w;
+          has = true;
         }
       }
       if ((uint64_t)gw + (uint64_t)W * (pos + n_need) >= total) exhausted = true;
-      if (lane == 0) ws[0] = pos + n_need;
-      const uint64_t fm = __ballot(fresh);
-      if (fm != 0) {  // new path ids for the fresh lanes, from the wave's pool (one atomic per 1024 ids)
-        const uint32_t nf = (uint32_t)__popcll(fm);
-        const uint32_t pn = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[1]);
-        const uint32_t pe = (uint32_t)__builtin_amdgcn_readfirstlane((int)ws[2]);
-        const uint32_t avail = pe - pn;
-        uint64_t nb = P;
-        if (avail < nf) {
-          if (lane == 0) ws[3] = (uint32_t)min((unsigned long long)P, atomicAdd(a.queue, 1024ull));
-          nb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)ws[3]);
-        }
-        const uint64_t ne = nb + 1024u < P ? nb + 1024u : P;
-        if (fresh) {
-          const uint32_t r2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-          const uint64_t id = r2 < avail ? (uint64_t)pn + r2 : nb + (r2 - avail);
-          PathState st;
-          if (id >= (r2 < avail ? (uint64_t)pe : ne)) {
-            w.hit[slot] = make_uint2(0u, (uint32_t)-3);
-          } else if (start_path<true>(SA, id, st)) {
-            ray = st.ray;
-            w.thr[slot] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
-            w.rng[slot] = st.rng;
-            w.pid[slot] = st.pid;
-            w.ray_o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.time);
-            w.ray_d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-            has = true;
-            ++n_consumed;
-          } else {
-            w.hit[slot] = make_uint2(0u, (uint32_t)-4);
-            ++n_consumed;
-          }
-        }
-        if (lane == 0) {
-          if (avail >= nf) {
-            ws[1] = pn + nf;
-          } else {
-            const uint64_t nn = nb + (nf - avail);
-            ws[1] = (uint32_t)(nn < ne ? nn : ne);
-            ws[2] = (uint32_t)ne;
-          }
-        }
-      }
+      if (lane == 0) wpos[wv] = pos + n_need;
     }
     if (__ballot(has) == 0) {
       if (exhausted) break;
@@ -1819,131 +1753,147 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
     has = false;
   }
   if (lane == 0 && nrays) atomicAdd(a.counters, nrays);
-  // path ids consumed (started or off the image): summed per workgroup, one atomic per workgroup
-  unsigned long long c = n_consumed;
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if (lane == 0) {
-    if (c) atomicAdd(&consumed, c);
-    w.wpool[gw] = make_uint2(ws[1], ws[2]);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && consumed) atomicAdd(reinterpret_cast<unsigned long long*>(w.cnt + 32), consumed);
 }
 
 __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) {
   constexpr uint32_t FEAT = F_SPHERES;
-  __shared__ uint32_t pre[17];
-  __shared__ uint32_t nap[2], base[2];
-  const uint32_t par = w.par;
+  __shared__ uint32_t pre[WF_SHARDS + 1];
+  __shared__ uint32_t nap, nfin, base_q, base_k;
+  __shared__ uint32_t fin_slots[1024];
+  __shared__ StartArgs start_lds[1];
+  const uint32_t par = w.par, sh = blockIdx.x & (WF_SHARDS - 1);
   if (threadIdx.x == 0) {
     wf_prefix(w, pre);
-    nap[0] = 0u;
-    nap[1] = 0u;
+    nap = 0u;
+    nfin = 0u;
+    fill_start_args(a, start_lds[0]);
   }
   __syncthreads();
-  const uint32_t total = pre[16];
+  const uint32_t total = w.init ? w.n_slots : pre[WF_SHARDS];
   if (blockIdx.x * 1024u >= total) return;  // whole block idle (uniform)
   const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
-  bool to_ray = false, to_free = false;
+  bool to_ray = false, fin = false;
   uint32_t slot = 0;
   if (i < total) {
-    bool fresh_item;
-    slot = wf_slot(w, pre, i, fresh_item);
+    slot = w.init ? i : wf_slot(w, pre, i);
+    fin = w.init != 0u;
+  }
+  if (i < total && !w.init) {
     const uint2 hv = w.hit[slot];
     const int32_t prim = (int32_t)hv.y;
-    if (prim == -4) {
-      to_free = true;
-    } else if (prim != -3) {
-      const DevScene& S = a.scene;
-      const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot], T4 = w.thr[slot];
-      Ray r;
-      r.o = mk(o4.x, o4.y, o4.z);
-      r.d = mk(d4.x, d4.y, d4.z);
-      r.time = o4.w;
-      const V3 T = mk(T4.x, T4.y, T4.z);
-      uint32_t depth = __float_as_uint(T4.w);
-      uint64_t rng = w.rng[slot];
-      const Best b{__uint_as_float(hv.x), 0u, prim, 0.0f, 0.0f};
-      bool done = false;
-      V3 L = mk(0.f, 0.f, 0.f);
-      if (b.prim < 0) {  // lib.rs:102-105 (a tripped guard, prim -2, shades as a miss; the error is reported)
-        L = mul(T, ld3(a.bg));
+    const DevScene& S = a.scene;
+    const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot], T4 = w.thr[slot];
+    Ray r;
+    r.o = mk(o4.x, o4.y, o4.z);
+    r.d = mk(d4.x, d4.y, d4.z);
+    r.time = o4.w;
+    const V3 T = mk(T4.x, T4.y, T4.z);
+    uint32_t depth = __float_as_uint(T4.w);
+    uint64_t rng = w.rng[slot];
+    const Best b{__uint_as_float(hv.x), 0u, prim, 0.0f, 0.0f};
+    bool done = false;
+    V3 L = mk(0.f, 0.f, 0.f);
+    if (b.prim < 0) {  // lib.rs:102-105 (a tripped guard, prim -2, shades as a miss; the error is reported)
+      L = mul(T, ld3(a.bg));
+      done = true;
+    } else {
+      const DevShade shd = S.shade[b.prim];
+      const Rec h = hit_record<FEAT>(S, r, b, shd.kind);
+      const uint32_t mt = shd.kind & 0xffu, mode = (shd.kind >> 8) & 0xfu;
+      const bool light = mt == MT_LIGHT, lam = mt == MT_LAMBERT, met = mt == MT_METAL;
+      V3 rs = mk(0.f, 0.f, 0.f);
+      if (lam || met) rs = rand_in_unit_sphere<true>(rng);  // vec3.rs:101-108
+      const V3 ud = unit(lam ? rs : r.d);
+      V3 att = mk(1.f, 1.f, 1.f);
+      if (met) {
+        att = ld3(shd.a);
+      } else if (light || lam) {
+        if (mode == SM_SOLID) att = ld3(shd.a);
+        else if (mode == SM_CHECKER)
+          att = checker_odd(shd.param * h.p.x, shd.param * h.p.y, shd.param * h.p.z) ? ld3(shd.a) : ld3(shd.b);
+      }
+      if (light) {
+        L = mul(T, att);
         done = true;
       } else {
-        const DevShade sh = S.shade[b.prim];
-        const Rec h = hit_record<FEAT>(S, r, b, sh.kind);
-        const uint32_t mt = sh.kind & 0xffu, mode = (sh.kind >> 8) & 0xfu;
-        const bool light = mt == MT_LIGHT, lam = mt == MT_LAMBERT, met = mt == MT_METAL;
-        V3 rs = mk(0.f, 0.f, 0.f);
-        if (lam || met) rs = rand_in_unit_sphere<true>(rng);  // vec3.rs:101-108
-        const V3 ud = unit(lam ? rs : r.d);
-        V3 att = mk(1.f, 1.f, 1.f);
-        if (met) {
-          att = ld3(sh.a);
-        } else if (light || lam) {
-          if (mode == SM_SOLID) att = ld3(sh.a);
-          else if (mode == SM_CHECKER)
-            att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a) : ld3(sh.b);
+        V3 dir = rs;
+        if (lam) {  // material.rs:42-56
+          dir = add(h.n, ud);
+          if (near_zero(dir)) dir = h.n;
+        } else if (met) {  // material.rs:78-95
+          dir = add(reflect(ud, h.n), scale(rs, shd.param));
+          done = !(dot(dir, h.n) > 0.0f);
+        } else {  // Dielectric, material.rs:116-142
+          const float ratio = h.front ? shd.a[0] : shd.param;
+          const float r0 = h.front ? shd.a[1] : shd.a[2];
+          const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
+          const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+          const bool cannot = (ratio * sin_t) > 1.0f;
+          if (cannot || reflectance(cos_t, r0) > gen_f32(rng)) dir = reflect(ud, h.n);
+          else dir = refract(ud, h.n, ratio);
         }
-        if (light) {
-          L = mul(T, att);
-          done = true;
-        } else {
-          V3 dir = rs;
-          if (lam) {  // material.rs:42-56
-            dir = add(h.n, ud);
-            if (near_zero(dir)) dir = h.n;
-          } else if (met) {  // material.rs:78-95
-            dir = add(reflect(ud, h.n), scale(rs, sh.param));
-            done = !(dot(dir, h.n) > 0.0f);
-          } else {  // Dielectric, material.rs:116-142
-            const float ratio = h.front ? sh.a[0] : sh.param;
-            const float r0 = h.front ? sh.a[1] : sh.a[2];
-            const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
-            const float sin_t = sqrtf(1.0f - cos_t * cos_t);
-            const bool cannot = (ratio * sin_t) > 1.0f;
-            if (cannot || reflectance(cos_t, r0) > gen_f32(rng)) dir = reflect(ud, h.n);
-            else dir = refract(ud, h.n, ratio);
-          }
-          const V3 T2 = mul(T, att);
-          if (!done) done = --depth == 0u;  // lib.rs:98-100
-          if (!done) {
-            w.ray_o[slot] = make_float4(h.p.x, h.p.y, h.p.z, r.time);
-            w.ray_d[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
-            w.thr[slot] = make_float4(T2.x, T2.y, T2.z, __uint_as_float(depth));
-            w.rng[slot] = rng;
-          }
+        const V3 T2 = mul(T, att);
+        if (!done) done = --depth == 0u;  // lib.rs:98-100
+        if (!done) {
+          w.ray_o[slot] = make_float4(h.p.x, h.p.y, h.p.z, r.time);
+          w.ray_d[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
+          w.thr[slot] = make_float4(T2.x, T2.y, T2.z, __uint_as_float(depth));
+          w.rng[slot] = rng;
         }
-      }
-      if (done) {
-        float* o = a.sbuf + (size_t)w.pid[slot] * 3u;
-        __builtin_nontemporal_store(L.x, o);
-        __builtin_nontemporal_store(L.y, o + 1);
-        __builtin_nontemporal_store(L.z, o + 2);
-        to_free = true;
-      } else {
-        to_ray = true;
       }
     }
+    if (done) {
+      float* o = a.sbuf + (size_t)w.pid[slot] * 3u;
+      __builtin_nontemporal_store(L.x, o);
+      __builtin_nontemporal_store(L.y, o + 1);
+      __builtin_nontemporal_store(L.z, o + 2);
+      fin = true;
+    } else {
+      to_ray = true;
+    }
   }
-  // appends: offsets from LDS counters, then one global atomic per queue for the block's shard
-  const uint32_t oray = to_ray ? atomicAdd(&nap[0], 1u) : 0u, ofree = to_free ? atomicAdd(&nap[1], 1u) : 0u;
+  // finished slots, compacted: new paths with full lanes
+  if (fin) fin_slots[atomicAdd(&nfin, 1u)] = slot;
   __syncthreads();
-  const uint32_t sh = blockIdx.x & (WF_SHARDS - 1);
-  if (threadIdx.x == 0) {
-    base[0] = nap[0] ? atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap[0]) : 0u;
-    base[1] = nap[1] ? atomicAdd(&w.cnt[16 + (1 - par) * 8 + sh], nap[1]) : 0u;
+  if (threadIdx.x == 0 && nfin) base_k = atomicAdd(&w.cnt[16 + sh], nfin);
+  __syncthreads();
+  if (threadIdx.x < nfin) {
+    const uint64_t P = a.n_paths;
+    slot = fin_slots[threadIdx.x];
+    uint64_t k = (uint64_t)base_k + threadIdx.x;
+    uint32_t ss = sh, tries = 0;
+    for (;;) {
+      const uint64_t id = k * WF_SHARDS + ss;
+      if (id >= P) {  // this dispenser is dry: the others may not be (slots move between shards)
+        if (++tries == WF_SHARDS) break;  // out of path ids everywhere: the slot retires
+        ss = (ss + 1u) & (WF_SHARDS - 1u);
+        k = atomicAdd(&w.cnt[16 + ss], 1u);
+        continue;
+      }
+      PathState st;
+      if (start_path<true>(start_lds[0], id, st)) {
+        w.thr[slot] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
+        w.rng[slot] = st.rng;
+        w.pid[slot] = st.pid;
+        w.ray_o[slot] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
+        w.ray_d[slot] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, 0.f);
+        to_ray = true;
+        break;
+      }
+      k = atomicAdd(&w.cnt[16 + ss], 1u);  // an id off the image (a partial tile): draw another (rare)
+    }
   }
+  // appends to the next ray queue: offsets from an LDS counter, one global atomic per block
+  const uint32_t oray = to_ray ? atomicAdd(&nap, 1u) : 0u;
   __syncthreads();
-  if (to_ray) w.rayq[1 - par][(size_t)sh * w.shard_cap + base[0] + oray] = slot;
-  if (to_free) w.freeq[1 - par][(size_t)sh * w.shard_cap + base[1] + ofree] = slot;
+  if (threadIdx.x == 0 && nap) base_q = atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap);
+  __syncthreads();
+  if (to_ray) w.rayq[1 - par][(size_t)sh * w.shard_cap + base_q + oray] = slot;
 }
 
-__global__ void wf_init_kernel(WfArgs w, uint32_t n_waves) {  // n_slots is a multiple of 8
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, per = w.n_slots / WF_SHARDS;
-  if (i < w.n_slots) w.freeq[0][(size_t)(i / per) * w.shard_cap + i % per] = i;  // shard s: slots [s per, (s + 1) per)
-  if (i < n_waves) w.wpool[i] = make_uint2(0u, 0u);
-  if (i < 34) w.cnt[i] = (i >= 16 && i < 24) ? per : 0u;
+__global__ void wf_init_kernel(WfArgs w) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 32) w.cnt[i] = 0u;
 }
 
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
@@ -2309,16 +2259,16 @@ int check_guard(DeviceCopy& c) {
 // pinned memory, and the chunk before it is checked (so the GPU always has a chunk queued): the pass is done
 // once no ray is queued and every path id has been handed out.
 static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
-  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21))) & ~7u;
-  const uint32_t cap = N / dev::WF_SHARDS + 1024u;  // a shard gets <= ceil(blocks / 8) blocks of 1024 items
+  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21))) & ~1023u;
+  // a shard receives the appends of every 8th shading block (<= 1024 each)
+  const uint32_t cap = ((N / 1024u + 7u) / 8u) * 1024u;
   constexpr int STACK = 16, BLK = 1024, NCAP = 144;
   auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
-  const uint32_t tblocks = (uint32_t)(per_cu * cus), n_waves = tblocks * (BLK / 64);
   const size_t qbytes = (size_t)dev::WF_SHARDS * cap * 4;
-  const size_t need = (size_t)N * (16 * 3 + 8 + 8 + 4) + 4 * qbytes + (size_t)n_waves * 8 + 256;
+  const size_t need = (size_t)N * (16 * 3 + 8 + 8 + 4) + 2 * qbytes + 256;
   if (need > c.wf_bytes) {
     if (c.wf_block) HIPCHK(hipFree(c.wf_block), "hipFree(wavefront)");
     c.wf_block = nullptr;
@@ -2342,18 +2292,19 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
   wa.hit = reinterpret_cast<uint2*>(p); p += (size_t)N * 8;
   wa.pid = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4;
   for (int k = 0; k < 2; ++k) { wa.rayq[k] = reinterpret_cast<uint32_t*>(p); p += qbytes; }
-  for (int k = 0; k < 2; ++k) { wa.freeq[k] = reinterpret_cast<uint32_t*>(p); p += qbytes; }
-  wa.wpool = reinterpret_cast<uint2*>(p); p += (size_t)n_waves * 8;
   wa.cnt = reinterpret_cast<uint32_t*>(p);
   wa.n_slots = N;
   wa.shard_cap = cap;
+  wa.par = 1;
+  wa.init = 1;
+  hipLaunchKernelGGL(dev::wf_init_kernel, dim3(1), dim3(64), 0, stream, wa);
+  const dim3 tgrid(per_cu * cus), sgrid(N / 1024);
+  // the first shading pass only starts a path in every slot; its appends go to ray queue 0
+  hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(1024), 0, stream, a, wa);
+  HIPCHK(hipGetLastError(), "wavefront start");
+  wa.init = 0;
   wa.par = 0;
-  const uint32_t ninit = std::max(N, n_waves);
-  hipLaunchKernelGGL(dev::wf_init_kernel, dim3((ninit + 255) / 256), dim3(256), 0, stream, wa, n_waves);
-  HIPCHK(hipGetLastError(), "wf_init_kernel");
-  const dim3 tgrid(tblocks), sgrid((N + 1023) / 1024);
   const uint32_t chunk = (uint32_t)std::max(1, env_int("RTW_WF_CHUNK", 16));
-  const uint64_t P = a.n_paths;
   for (uint32_t ch = 0;; ++ch) {
     for (uint32_t k = 0; k < chunk; ++k) {
       hipLaunchKernelGGL(trace, tgrid, dim3(BLK), 0, stream, a, wa);
@@ -2361,17 +2312,15 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
       wa.par ^= 1u;
     }
     HIPCHK(hipGetLastError(), "wavefront launches");
-    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // [0..7] next rayq shard counts, [8..9] ids consumed
+    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // the next iteration's ray-queue shard counts
     HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par * 8, 32, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
-    HIPCHK(hipMemcpyAsync(hb + 8, wa.cnt + 32, 8, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
     HIPCHK(hipEventRecord(static_cast<hipEvent_t>(c.wf_ev[ch & 1u]), stream), "hipEventRecord");
     if (ch >= 1) {
       HIPCHK(hipEventSynchronize(static_cast<hipEvent_t>(c.wf_ev[(ch - 1) & 1u])), "wavefront progress");
       const uint32_t* pb = c.wf_host + 32 * ((ch - 1) & 1u);
       uint64_t rays = 0;
       for (int s = 0; s < 8; ++s) rays += pb[s];
-      const uint64_t consumed = (uint64_t)pb[8] | ((uint64_t)pb[9] << 32);
-      if (rays == 0 && consumed >= P) break;  // every path id started (or off the image) and no ray left
+      if (rays == 0) break;  // every slot has run out of path ids
     }
     if (ch > (1u << 22)) return fail(RTW_EINVAL, "wavefront: no progress");
   }
