@@ -1857,9 +1857,11 @@ __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) 
   __syncthreads();
   if (threadIdx.x == 0 && nfin) base_k = atomicAdd(&w.cnt[16 + sh], nfin);
   __syncthreads();
+  bool to_ray2 = false;  // this thread's new path (its own scattered ray, if any, is `slot` / `to_ray`)
+  uint32_t slot2 = 0;
   if (threadIdx.x < nfin) {
     const uint64_t P = a.n_paths;
-    slot = fin_slots[threadIdx.x];
+    slot2 = fin_slots[threadIdx.x];
     uint64_t k = (uint64_t)base_k + threadIdx.x;
     uint32_t ss = sh, tries = 0;
     for (;;) {
@@ -1872,23 +1874,25 @@ __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) 
       }
       PathState st;
       if (start_path<true>(start_lds[0], id, st)) {
-        w.thr[slot] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
-        w.rng[slot] = st.rng;
-        w.pid[slot] = st.pid;
-        w.ray_o[slot] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
-        w.ray_d[slot] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, 0.f);
-        to_ray = true;
+        w.thr[slot2] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
+        w.rng[slot2] = st.rng;
+        w.pid[slot2] = st.pid;
+        w.ray_o[slot2] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
+        w.ray_d[slot2] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, 0.f);
+        to_ray2 = true;
         break;
       }
       k = atomicAdd(&w.cnt[16 + ss], 1u);  // an id off the image (a partial tile): draw another (rare)
     }
   }
   // appends to the next ray queue: offsets from an LDS counter, one global atomic per block
-  const uint32_t oray = to_ray ? atomicAdd(&nap, 1u) : 0u;
+  const uint32_t oray = to_ray ? atomicAdd(&nap, 1u) : 0u, oray2 = to_ray2 ? atomicAdd(&nap, 1u) : 0u;
   __syncthreads();
   if (threadIdx.x == 0 && nap) base_q = atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap);
   __syncthreads();
-  if (to_ray) w.rayq[1 - par][(size_t)sh * w.shard_cap + base_q + oray] = slot;
+  uint32_t* const q = w.rayq[1 - par] + (size_t)sh * w.shard_cap + base_q;
+  if (to_ray) q[oray] = slot;
+  if (to_ray2) q[oray2] = slot2;
 }
 
 __global__ void wf_init_kernel(WfArgs w) {
