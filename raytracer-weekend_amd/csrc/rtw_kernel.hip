@@ -1640,39 +1640,44 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
 
 // ---- wavefront prototype (knob RTW_WAVEFRONT=1): the megakernel's loop split across
 // kernels by phase, so that every wave of a phase works on rays of that phase only.  Each iteration:
-//   wf_trace_kernel (persistent, LDS node table): wave gw of W takes items gw, gw + W, gw + 2W, ... of this
-//     iteration's ray queue (no atomics), traces them with the megakernel's resumable walk, and stores
-//     (t, prim) per slot; a lane whose query is done is refilled at once (no shading phase to wait for).
-//   wf_shade_kernel (one thread per item, 1024-thread blocks): the megakernel's shading body for the slot's
-//     hit; a scattered ray goes to the next ray queue; a finished path writes its sample, and the block's
-//     finished slots, compacted in LDS, start new paths with full lanes (start_path; path ids 8 k + shard
-//     from one of 8 dispensers, one atomic per block) and join the next ray queue too.
-//   Queue appends are counted in LDS: one global atomic per block, into one of 8 queue shards (block index
-//   mod 8).  The frame is done when an iteration leaves the ray queue empty (every slot out of path ids).
-// (The first version dispensed items and appended with one atomic per wave on one address each: ~100 K
-// same-address atomics per iteration at ~13 ns each made it 15x slower than the megakernel, r04b / r04c.)
-// Slot state lives in global memory (SoA, ~80 B per slot with the queues; RTW_WF_SLOTS slots).  Pixels
-// depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
+//   wf_trace_kernel (persistent, LDS node table): wave gw of W takes the contiguous items
+//     [gw C, (gw + 1) C) of this iteration's ray queue (C = ceil(total / W); no atomics), traces them with the
+//     megakernel's resumable walk and stores (t, prim) per item; a lane whose query is done is refilled at
+//     once (no shading phase to wait for).
+//   wf_shade_kernel (one thread per item, 1024-thread blocks): the megakernel's shading body for the item's
+//     hit; a scattered ray is appended to the next queue with its path state; a finished path writes its
+//     sample, and the block's finished items, compacted in LDS, start new paths with full lanes (start_path;
+//     path ids 8 k + shard from one of 8 dispensers, one atomic per block) appended the same way.
+//   Appends are counted in LDS: one global atomic per block into one of 8 queue shards (block index mod 8),
+//   and a block's appends are one contiguous, coalesced range.  The queues hold the ray and path state
+//   themselves (64 B per entry, in queue order), so every access is coalesced.  The frame is done when an
+//   iteration leaves the queue empty (every dispenser dry).
+// Versions: v1 dispensed items and appended with one atomic per wave on one address each (~100 K same-address
+// atomics per iteration at ~13 ns: 15x slower than the megakernel, r04b / r04c); v3 kept the state in fixed
+// slots indexed through the queues (every load and store a 64-line gather: 6x slower, r04e).
+// Pixels depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
 constexpr uint32_t WF_SHARDS = 8;
+struct WfQueue {
+  float4* o_t;    // ray origin, time
+  float4* d_dep;  // ray direction, remaining depth (bits)
+  float4* T_pid;  // throughput, path id (bits)
+  uint2* rng;     // the path's xoroshiro64* state
+};
 struct WfArgs {
-  float4* ray_o;       // o.xyz, time
-  float4* ray_d;       // d.xyz, -
-  float4* thr;         // T.xyz, remaining depth (bits)
-  uint64_t* rng;       // the path's xoroshiro64* state
-  uint32_t* pid;       // path id within the pass
-  uint2* hit;          // (t bits, prim)
-  uint32_t* rayq[2];   // [shard][shard_cap] slots with a ray to trace (parity p reads [p], shading appends to [1 - p])
-  uint32_t* cnt;       // [p * 8 + s] ray queue shard counts, [16 + s] path-id dispensers (k of pid = 8 k + s)
+  WfQueue q[2];        // [shard][shard_cap] entries; parity p reads q[p], shading appends to q[1 - p]
+  uint2* hit;          // per entry of the queue being traced: (t bits, prim)
+  uint32_t* cnt;       // [p * 8 + s] queue shard counts, [16 + s] path-id dispensers (k of pid = 8 k + s)
   uint32_t n_slots, shard_cap;
   uint32_t par;
-  uint32_t init;       // 1: wf_shade_kernel only starts a path in every slot (items = all slots)
+  uint32_t init;       // 1: wf_shade_kernel only starts n_slots paths
 };
 
-__device__ __forceinline__ uint32_t wf_slot(const WfArgs& w, const uint32_t* pre, uint32_t k) {
+// item k of the queue (shards in order; pre[0..8] their prefix counts) -> its entry index
+__device__ __forceinline__ uint32_t wf_entry(const WfArgs& w, const uint32_t* pre, uint32_t k) {
   uint32_t q = 0;
 #pragma unroll
   for (int s = 1; s < (int)WF_SHARDS; ++s) q += k >= pre[s] ? 1u : 0u;
-  return w.rayq[w.par][(size_t)q * w.shard_cap + (k - pre[q])];
+  return q * w.shard_cap + (k - pre[q]);
 }
 __device__ __forceinline__ void wf_prefix(const WfArgs& w, uint32_t* pre) {  // one thread of the block
   uint32_t t = 0;
@@ -1699,20 +1704,23 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
   const uint32_t gw = blockIdx.x * (BLK / 64) + wv, W = gridDim.x * (BLK / 64);
   if (threadIdx.x == 0) wf_prefix(w, pre);
   if (blockIdx.x == 0 && threadIdx.x < WF_SHARDS) w.cnt[(1 - par) * 8 + threadIdx.x] = 0u;  // the coming appends
-  if (lane == 0) wpos[wv] = 0u;
+  __syncthreads();
+  const uint32_t total = pre[WF_SHARDS], C = (total + W - 1) / W;
+  const uint32_t first = min(total, gw * C), last = min(total, first + C);  // this wave's items
+  if (lane == 0) wpos[wv] = first;
   __syncthreads();
   uint16_t* stk16 = stk16_all + threadIdx.x;
   const DevScene& S = a.scene;
-  const uint32_t total = pre[WF_SHARDS];
+  const WfQueue& Q = w.q[par];
   uint32_t cnt[15];
-  bool exhausted = (uint64_t)gw >= total, has = false;
+  bool exhausted = first >= last, has = false;
   TraceState ts;
   ts.on = false;
   Ray ray;
   ray.o = mk(0.f, 0.f, 0.f);
   ray.d = ray.o;
   ray.time = 0.f;
-  uint32_t slot = 0;
+  uint32_t ent = 0;
   unsigned long long nrays = 0;
   for (;;) {
     const uint64_t need = __ballot(!has);
@@ -1721,18 +1729,15 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)wpos[wv]);
-      if (!has) {
-        const uint64_t item = (uint64_t)gw + (uint64_t)W * (pos + rank);
-        if (item < total) {
-          slot = wf_slot(w, pre, (uint32_t)item);
-          const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot];
-          ray.o = mk(o4.x, o4.y, o4.z);
-          ray.d = mk(d4.x, d4.y, d4.z);
-          ray.time = o4.w;
-          has = true;
-        }
+      if (!has && pos + rank < last) {
+        ent = wf_entry(w, pre, pos + rank);
+        const float4 o4 = Q.o_t[ent], d4 = Q.d_dep[ent];
+        ray.o = mk(o4.x, o4.y, o4.z);
+        ray.d = mk(d4.x, d4.y, d4.z);
+        ray.time = o4.w;
+        has = true;
       }
-      if ((uint64_t)gw + (uint64_t)W * (pos + n_need) >= total) exhausted = true;
+      if (pos + n_need >= last) exhausted = true;
       if (lane == 0) wpos[wv] = pos + n_need;
     }
     if (__ballot(has) == 0) {
@@ -1749,7 +1754,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))
                                                           a.err, nullptr, nodes_lds, stk16);
     if (ts.node >= 0 || ts.sp > 0) continue;  // suspended: resume next round
     ts.on = false;
-    w.hit[slot] = make_uint2(__float_as_uint(ts.b.t), (uint32_t)ts.b.prim);
+    w.hit[ent] = make_uint2(__float_as_uint(ts.b.t), (uint32_t)ts.b.prim);
     has = false;
   }
   if (lane == 0 && nrays) atomicAdd(a.counters, nrays);
@@ -1759,7 +1764,6 @@ __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) 
   constexpr uint32_t FEAT = F_SPHERES;
   __shared__ uint32_t pre[WF_SHARDS + 1];
   __shared__ uint32_t nap, nfin, base_q, base_k;
-  __shared__ uint32_t fin_slots[1024];
   __shared__ StartArgs start_lds[1];
   const uint32_t par = w.par, sh = blockIdx.x & (WF_SHARDS - 1);
   if (threadIdx.x == 0) {
@@ -1772,24 +1776,27 @@ __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) 
   const uint32_t total = w.init ? w.n_slots : pre[WF_SHARDS];
   if (blockIdx.x * 1024u >= total) return;  // whole block idle (uniform)
   const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
-  bool to_ray = false, fin = false;
-  uint32_t slot = 0;
-  if (i < total) {
-    slot = w.init ? i : wf_slot(w, pre, i);
-    fin = w.init != 0u;
-  }
+  bool to_q = false, fin = false;
+  float4 o_t, d_dep, T_pid;
+  uint2 rg;
+  if (i < total && w.init) fin = true;
   if (i < total && !w.init) {
-    const uint2 hv = w.hit[slot];
+    const WfQueue& Q = w.q[par];
+    const uint32_t e = wf_entry(w, pre, i);
+    const uint2 hv = w.hit[e];
     const int32_t prim = (int32_t)hv.y;
     const DevScene& S = a.scene;
-    const float4 o4 = w.ray_o[slot], d4 = w.ray_d[slot], T4 = w.thr[slot];
+    o_t = Q.o_t[e];
+    d_dep = Q.d_dep[e];
+    T_pid = Q.T_pid[e];
     Ray r;
-    r.o = mk(o4.x, o4.y, o4.z);
-    r.d = mk(d4.x, d4.y, d4.z);
-    r.time = o4.w;
-    const V3 T = mk(T4.x, T4.y, T4.z);
-    uint32_t depth = __float_as_uint(T4.w);
-    uint64_t rng = w.rng[slot];
+    r.o = mk(o_t.x, o_t.y, o_t.z);
+    r.d = mk(d_dep.x, d_dep.y, d_dep.z);
+    r.time = o_t.w;
+    const V3 T = mk(T_pid.x, T_pid.y, T_pid.z);
+    uint32_t depth = __float_as_uint(d_dep.w);
+    const uint2 r2 = Q.rng[e];
+    uint64_t rng = (uint64_t)r2.x | ((uint64_t)r2.y << 32);
     const Best b{__uint_as_float(hv.x), 0u, prim, 0.0f, 0.0f};
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
@@ -1834,65 +1841,68 @@ __global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) 
         }
         const V3 T2 = mul(T, att);
         if (!done) done = --depth == 0u;  // lib.rs:98-100
-        if (!done) {
-          w.ray_o[slot] = make_float4(h.p.x, h.p.y, h.p.z, r.time);
-          w.ray_d[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
-          w.thr[slot] = make_float4(T2.x, T2.y, T2.z, __uint_as_float(depth));
-          w.rng[slot] = rng;
-        }
+        o_t = make_float4(h.p.x, h.p.y, h.p.z, r.time);
+        d_dep = make_float4(dir.x, dir.y, dir.z, __uint_as_float(depth));
+        T_pid = make_float4(T2.x, T2.y, T2.z, T_pid.w);
+        rg = make_uint2((uint32_t)rng, (uint32_t)(rng >> 32));
       }
     }
     if (done) {
-      float* o = a.sbuf + (size_t)w.pid[slot] * 3u;
+      float* o = a.sbuf + (size_t)__float_as_uint(T_pid.w) * 3u;
       __builtin_nontemporal_store(L.x, o);
       __builtin_nontemporal_store(L.y, o + 1);
       __builtin_nontemporal_store(L.z, o + 2);
       fin = true;
     } else {
-      to_ray = true;
+      to_q = true;
     }
   }
-  // finished slots, compacted: new paths with full lanes
-  if (fin) fin_slots[atomicAdd(&nfin, 1u)] = slot;
+  // finished paths: the block's count decides how many new ids it draws (one atomic); the first nfin threads
+  // start them (full lanes; a thread may append its own scattered ray and a new path)
+  if (fin) atomicAdd(&nfin, 1u);
   __syncthreads();
   if (threadIdx.x == 0 && nfin) base_k = atomicAdd(&w.cnt[16 + sh], nfin);
   __syncthreads();
-  bool to_ray2 = false;  // this thread's new path (its own scattered ray, if any, is `slot` / `to_ray`)
-  uint32_t slot2 = 0;
+  bool to_q2 = false;
+  PathState st;
   if (threadIdx.x < nfin) {
     const uint64_t P = a.n_paths;
-    slot2 = fin_slots[threadIdx.x];
     uint64_t k = (uint64_t)base_k + threadIdx.x;
     uint32_t ss = sh, tries = 0;
     for (;;) {
       const uint64_t id = k * WF_SHARDS + ss;
-      if (id >= P) {  // this dispenser is dry: the others may not be (slots move between shards)
-        if (++tries == WF_SHARDS) break;  // out of path ids everywhere: the slot retires
+      if (id >= P) {  // this dispenser is dry: the others may not be
+        if (++tries == WF_SHARDS) break;  // out of path ids everywhere
         ss = (ss + 1u) & (WF_SHARDS - 1u);
         k = atomicAdd(&w.cnt[16 + ss], 1u);
         continue;
       }
-      PathState st;
       if (start_path<true>(start_lds[0], id, st)) {
-        w.thr[slot2] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.depth));
-        w.rng[slot2] = st.rng;
-        w.pid[slot2] = st.pid;
-        w.ray_o[slot2] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
-        w.ray_d[slot2] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, 0.f);
-        to_ray2 = true;
+        to_q2 = true;
         break;
       }
       k = atomicAdd(&w.cnt[16 + ss], 1u);  // an id off the image (a partial tile): draw another (rare)
     }
   }
-  // appends to the next ray queue: offsets from an LDS counter, one global atomic per block
-  const uint32_t oray = to_ray ? atomicAdd(&nap, 1u) : 0u, oray2 = to_ray2 ? atomicAdd(&nap, 1u) : 0u;
+  // appends to the next queue: offsets from an LDS counter, one global atomic per block, one contiguous range
+  const uint32_t oq = to_q ? atomicAdd(&nap, 1u) : 0u, oq2 = to_q2 ? atomicAdd(&nap, 1u) : 0u;
   __syncthreads();
   if (threadIdx.x == 0 && nap) base_q = atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap);
   __syncthreads();
-  uint32_t* const q = w.rayq[1 - par] + (size_t)sh * w.shard_cap + base_q;
-  if (to_ray) q[oray] = slot;
-  if (to_ray2) q[oray2] = slot2;
+  const WfQueue& O = w.q[1 - par];
+  const uint32_t ob = sh * w.shard_cap + base_q;
+  if (to_q) {
+    O.o_t[ob + oq] = o_t;
+    O.d_dep[ob + oq] = d_dep;
+    O.T_pid[ob + oq] = T_pid;
+    O.rng[ob + oq] = rg;
+  }
+  if (to_q2) {
+    O.o_t[ob + oq2] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
+    O.d_dep[ob + oq2] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, __uint_as_float(st.depth));
+    O.T_pid[ob + oq2] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.pid));
+    O.rng[ob + oq2] = make_uint2((uint32_t)st.rng, (uint32_t)(st.rng >> 32));
+  }
 }
 
 __global__ void wf_init_kernel(WfArgs w) {
@@ -2264,15 +2274,16 @@ int check_guard(DeviceCopy& c) {
 // once no ray is queued and every path id has been handed out.
 static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
   const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21))) & ~1023u;
-  // a shard receives the appends of every 8th shading block (<= 1024 each)
+  // a shard receives the appends of every 8th shading block (<= 2 x 1024 each: a scattered ray + a new path
+  // per thread at most, but no more than the block's 1024 items + its new paths, which are <= its finished ones)
   const uint32_t cap = ((N / 1024u + 7u) / 8u) * 1024u;
   constexpr int STACK = 16, BLK = 1024, NCAP = 144;
   auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
-  const size_t qbytes = (size_t)dev::WF_SHARDS * cap * 4;
-  const size_t need = (size_t)N * (16 * 3 + 8 + 8 + 4) + 2 * qbytes + 256;
+  const size_t E = (size_t)dev::WF_SHARDS * cap;  // entries per queue
+  const size_t need = 2 * E * (16 * 3 + 8) + E * 8 + 256;
   if (need > c.wf_bytes) {
     if (c.wf_block) HIPCHK(hipFree(c.wf_block), "hipFree(wavefront)");
     c.wf_block = nullptr;
@@ -2289,13 +2300,13 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
     }
   uint8_t* p = static_cast<uint8_t*>(c.wf_block);
   dev::WfArgs wa;
-  wa.ray_o = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
-  wa.ray_d = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
-  wa.thr = reinterpret_cast<float4*>(p); p += (size_t)N * 16;
-  wa.rng = reinterpret_cast<uint64_t*>(p); p += (size_t)N * 8;
-  wa.hit = reinterpret_cast<uint2*>(p); p += (size_t)N * 8;
-  wa.pid = reinterpret_cast<uint32_t*>(p); p += (size_t)N * 4;
-  for (int k = 0; k < 2; ++k) { wa.rayq[k] = reinterpret_cast<uint32_t*>(p); p += qbytes; }
+  for (int k = 0; k < 2; ++k) {
+    wa.q[k].o_t = reinterpret_cast<float4*>(p); p += E * 16;
+    wa.q[k].d_dep = reinterpret_cast<float4*>(p); p += E * 16;
+    wa.q[k].T_pid = reinterpret_cast<float4*>(p); p += E * 16;
+    wa.q[k].rng = reinterpret_cast<uint2*>(p); p += E * 8;
+  }
+  wa.hit = reinterpret_cast<uint2*>(p); p += E * 8;
   wa.cnt = reinterpret_cast<uint32_t*>(p);
   wa.n_slots = N;
   wa.shard_cap = cap;
@@ -2303,7 +2314,7 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
   wa.init = 1;
   hipLaunchKernelGGL(dev::wf_init_kernel, dim3(1), dim3(64), 0, stream, wa);
   const dim3 tgrid(per_cu * cus), sgrid(N / 1024);
-  // the first shading pass only starts a path in every slot; its appends go to ray queue 0
+  // the first shading pass only starts N paths; its appends go to queue 0
   hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(1024), 0, stream, a, wa);
   HIPCHK(hipGetLastError(), "wavefront start");
   wa.init = 0;
@@ -2316,7 +2327,7 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
       wa.par ^= 1u;
     }
     HIPCHK(hipGetLastError(), "wavefront launches");
-    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // the next iteration's ray-queue shard counts
+    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // the next iteration's queue shard counts
     HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par * 8, 32, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
     HIPCHK(hipEventRecord(static_cast<hipEvent_t>(c.wf_ev[ch & 1u]), stream), "hipEventRecord");
     if (ch >= 1) {
@@ -2324,7 +2335,7 @@ static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
       const uint32_t* pb = c.wf_host + 32 * ((ch - 1) & 1u);
       uint64_t rays = 0;
       for (int s = 0; s < 8; ++s) rays += pb[s];
-      if (rays == 0) break;  // every slot has run out of path ids
+      if (rays == 0) break;  // every dispenser is dry and every path done
     }
     if (ch > (1u << 22)) return fail(RTW_EINVAL, "wavefront: no progress");
   }
