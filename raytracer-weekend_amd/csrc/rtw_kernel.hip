@@ -1638,277 +1638,8 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   o[2] = z;
 }
 
-// ---- wavefront prototype (knob RTW_WAVEFRONT=1): the megakernel's loop split across
-// kernels by phase, so that every wave of a phase works on rays of that phase only.  Each iteration:
-//   wf_trace_kernel (persistent, LDS node table): wave gw of W takes the contiguous items
-//     [gw C, (gw + 1) C) of this iteration's ray queue (C = ceil(total / W); no atomics), traces them with the
-//     megakernel's resumable walk and stores (t, prim) per item; a lane whose query is done is refilled at
-//     once (no shading phase to wait for).
-//   wf_shade_kernel (one thread per item, 1024-thread blocks): the megakernel's shading body for the item's
-//     hit; a scattered ray is appended to the next queue with its path state; a finished path writes its
-//     sample, and the block's finished items, compacted in LDS, start new paths with full lanes (start_path;
-//     path ids 8 k + shard from one of 8 dispensers, one atomic per block) appended the same way.
-//   Appends are counted in LDS: one global atomic per block into one of 8 queue shards (block index mod 8),
-//   and a block's appends are one contiguous, coalesced range.  The queues hold the ray and path state
-//   themselves (64 B per entry, in queue order), so every access is coalesced.  The frame is done when an
-//   iteration leaves the queue empty (every dispenser dry).
-// Versions: v1 dispensed items and appended with one atomic per wave on one address each (~100 K same-address
-// atomics per iteration at ~13 ns: 15x slower than the megakernel, r04b / r04c); v3 kept the state in fixed
-// slots indexed through the queues (every load and store a 64-line gather: 6x slower, r04e).
-// Pixels depend only on (seed, pixel, sample), so the image is the megakernel's, bit for bit.
-constexpr uint32_t WF_SHARDS = 8;
-struct WfQueue {
-  float4* o_t;    // ray origin, time
-  float4* d_dep;  // ray direction, remaining depth (bits)
-  float4* T_pid;  // throughput, path id (bits)
-  uint2* rng;     // the path's xoroshiro64* state
-};
-struct WfArgs {
-  WfQueue q[2];        // [shard][shard_cap] entries; parity p reads q[p], shading appends to q[1 - p]
-  uint2* hit;          // per entry of the queue being traced: (t bits, prim)
-  uint32_t* cnt;       // [p * 8 + s] queue shard counts, [16 + s] path-id dispensers (k of pid = 8 k + s)
-  uint32_t n_slots, shard_cap;
-  uint32_t par;
-  uint32_t init;       // 1: wf_shade_kernel only starts n_slots paths
-};
-
-// item k of the queue (shards in order; pre[0..8] their prefix counts) -> its entry index
-__device__ __forceinline__ uint32_t wf_entry(const WfArgs& w, const uint32_t* pre, uint32_t k) {
-  uint32_t q = 0;
-#pragma unroll
-  for (int s = 1; s < (int)WF_SHARDS; ++s) q += k >= pre[s] ? 1u : 0u;
-  return q * w.shard_cap + (k - pre[q]);
-}
-__device__ __forceinline__ void wf_prefix(const WfArgs& w, uint32_t* pre) {  // one thread of the block
-  uint32_t t = 0;
-  for (uint32_t s = 0; s < WF_SHARDS; ++s) {
-    pre[s] = t;
-    t += w.cnt[w.par * 8 + s];
-  }
-  pre[WF_SHARDS] = t;
-}
-
-#ifndef WF_OCC
-#define WF_OCC 8  // waves / SIMD of wf_trace_kernel
-#endif
-template <int STACK, int BLK, int NCAP>
-__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WF_OCC, 8))) void wf_trace_kernel(RenderArgs a, WfArgs w) {
-  constexpr uint32_t FEAT = F_SPHERES;
-  __shared__ uint16_t stk16_all[STACK * BLK];
-  __shared__ float4 nodes_lds[NCAP * 8];
-  __shared__ uint32_t pre[WF_SHARDS + 1];
-  __shared__ uint32_t wpos[BLK / 64];
-  for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * 8u; k += BLK)
-    nodes_lds[k] = reinterpret_cast<const float4*>(a.scene.nodes)[k];
-  const uint32_t par = w.par, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t gw = blockIdx.x * (BLK / 64) + wv, W = gridDim.x * (BLK / 64);
-  if (threadIdx.x == 0) wf_prefix(w, pre);
-  if (blockIdx.x == 0 && threadIdx.x < WF_SHARDS) w.cnt[(1 - par) * 8 + threadIdx.x] = 0u;  // the coming appends
-  __syncthreads();
-  const uint32_t total = pre[WF_SHARDS], C = (total + W - 1) / W;
-  const uint32_t first = min(total, gw * C), last = min(total, first + C);  // this wave's items
-  if (lane == 0) wpos[wv] = first;
-  __syncthreads();
-  uint16_t* stk16 = stk16_all + threadIdx.x;
-  const DevScene& S = a.scene;
-  const WfQueue& Q = w.q[par];
-  uint32_t cnt[15];
-  bool exhausted = first >= last, has = false;
-  TraceState ts;
-  ts.on = false;
-  Ray ray;
-  ray.o = mk(0.f, 0.f, 0.f);
-  ray.d = ray.o;
-  ray.time = 0.f;
-  uint32_t ent = 0;
-  unsigned long long nrays = 0;
-  for (;;) {
-    const uint64_t need = __ballot(!has);
-    if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
-      const uint32_t n_need = (uint32_t)__popcll(need);
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)wpos[wv]);
-      if (!has && pos + rank < last) {
-        ent = wf_entry(w, pre, pos + rank);
-        const float4 o4 = Q.o_t[ent], d4 = Q.d_dep[ent];
-        ray.o = mk(o4.x, o4.y, o4.z);
-        ray.d = mk(d4.x, d4.y, d4.z);
-        ray.time = o4.w;
-        has = true;
-      }
-      if (pos + n_need >= last) exhausted = true;
-      if (lane == 0) wpos[wv] = pos + n_need;
-    }
-    if (__ballot(has) == 0) {
-      if (exhausted) break;
-      continue;
-    }
-    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
-    if (!has) continue;
-    if (!ts.on) trace_begin<false, FEAT>(S, ray, ts, cnt, 0);
-    const uint32_t act = (uint32_t)__popcll(__ballot(1));
-    const uint32_t quota = (act * a.quota16 + 15u) >> 4;
-    const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
-    trace_run<false, STACK, false, FEAT, BLK, NCAP, false>(S, ray, ts, nullptr, nullptr, 0u, cnt, quota, leaf_thr, 0,
-                                                          a.err, nullptr, nodes_lds, stk16);
-    if (ts.node >= 0 || ts.sp > 0) continue;  // suspended: resume next round
-    ts.on = false;
-    w.hit[ent] = make_uint2(__float_as_uint(ts.b.t), (uint32_t)ts.b.prim);
-    has = false;
-  }
-  if (lane == 0 && nrays) atomicAdd(a.counters, nrays);
-}
-
-__global__ __launch_bounds__(1024) void wf_shade_kernel(RenderArgs a, WfArgs w) {
-  constexpr uint32_t FEAT = F_SPHERES;
-  __shared__ uint32_t pre[WF_SHARDS + 1];
-  __shared__ uint32_t nap, nfin, base_q, base_k;
-  __shared__ StartArgs start_lds[1];
-  const uint32_t par = w.par, sh = blockIdx.x & (WF_SHARDS - 1);
-  if (threadIdx.x == 0) {
-    wf_prefix(w, pre);
-    nap = 0u;
-    nfin = 0u;
-    fill_start_args(a, start_lds[0]);
-  }
-  __syncthreads();
-  const uint32_t total = w.init ? w.n_slots : pre[WF_SHARDS];
-  if (blockIdx.x * 1024u >= total) return;  // whole block idle (uniform)
-  const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
-  bool to_q = false, fin = false;
-  float4 o_t, d_dep, T_pid;
-  uint2 rg;
-  if (i < total && w.init) fin = true;
-  if (i < total && !w.init) {
-    const WfQueue& Q = w.q[par];
-    const uint32_t e = wf_entry(w, pre, i);
-    const uint2 hv = w.hit[e];
-    const int32_t prim = (int32_t)hv.y;
-    const DevScene& S = a.scene;
-    o_t = Q.o_t[e];
-    d_dep = Q.d_dep[e];
-    T_pid = Q.T_pid[e];
-    Ray r;
-    r.o = mk(o_t.x, o_t.y, o_t.z);
-    r.d = mk(d_dep.x, d_dep.y, d_dep.z);
-    r.time = o_t.w;
-    const V3 T = mk(T_pid.x, T_pid.y, T_pid.z);
-    uint32_t depth = __float_as_uint(d_dep.w);
-    const uint2 r2 = Q.rng[e];
-    uint64_t rng = (uint64_t)r2.x | ((uint64_t)r2.y << 32);
-    const Best b{__uint_as_float(hv.x), 0u, prim, 0.0f, 0.0f};
-    bool done = false;
-    V3 L = mk(0.f, 0.f, 0.f);
-    if (b.prim < 0) {  // lib.rs:102-105 (a tripped guard, prim -2, shades as a miss; the error is reported)
-      L = mul(T, ld3(a.bg));
-      done = true;
-    } else {
-      const DevShade shd = S.shade[b.prim];
-      const Rec h = hit_record<FEAT>(S, r, b, shd.kind);
-      const uint32_t mt = shd.kind & 0xffu, mode = (shd.kind >> 8) & 0xfu;
-      const bool light = mt == MT_LIGHT, lam = mt == MT_LAMBERT, met = mt == MT_METAL;
-      V3 rs = mk(0.f, 0.f, 0.f);
-      if (lam || met) rs = rand_in_unit_sphere<true>(rng);  // vec3.rs:101-108
-      const V3 ud = unit(lam ? rs : r.d);
-      V3 att = mk(1.f, 1.f, 1.f);
-      if (met) {
-        att = ld3(shd.a);
-      } else if (light || lam) {
-        if (mode == SM_SOLID) att = ld3(shd.a);
-        else if (mode == SM_CHECKER)
-          att = checker_odd(shd.param * h.p.x, shd.param * h.p.y, shd.param * h.p.z) ? ld3(shd.a) : ld3(shd.b);
-      }
-      if (light) {
-        L = mul(T, att);
-        done = true;
-      } else {
-        V3 dir = rs;
-        if (lam) {  // material.rs:42-56
-          dir = add(h.n, ud);
-          if (near_zero(dir)) dir = h.n;
-        } else if (met) {  // material.rs:78-95
-          dir = add(reflect(ud, h.n), scale(rs, shd.param));
-          done = !(dot(dir, h.n) > 0.0f);
-        } else {  // Dielectric, material.rs:116-142
-          const float ratio = h.front ? shd.a[0] : shd.param;
-          const float r0 = h.front ? shd.a[1] : shd.a[2];
-          const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
-          const float sin_t = sqrtf(1.0f - cos_t * cos_t);
-          const bool cannot = (ratio * sin_t) > 1.0f;
-          if (cannot || reflectance(cos_t, r0) > gen_f32(rng)) dir = reflect(ud, h.n);
-          else dir = refract(ud, h.n, ratio);
-        }
-        const V3 T2 = mul(T, att);
-        if (!done) done = --depth == 0u;  // lib.rs:98-100
-        o_t = make_float4(h.p.x, h.p.y, h.p.z, r.time);
-        d_dep = make_float4(dir.x, dir.y, dir.z, __uint_as_float(depth));
-        T_pid = make_float4(T2.x, T2.y, T2.z, T_pid.w);
-        rg = make_uint2((uint32_t)rng, (uint32_t)(rng >> 32));
-      }
-    }
-    if (done) {
-      float* o = a.sbuf + (size_t)__float_as_uint(T_pid.w) * 3u;
-      __builtin_nontemporal_store(L.x, o);
-      __builtin_nontemporal_store(L.y, o + 1);
-      __builtin_nontemporal_store(L.z, o + 2);
-      fin = true;
-    } else {
-      to_q = true;
-    }
-  }
-  // finished paths: the block's count decides how many new ids it draws (one atomic); the first nfin threads
-  // start them (full lanes; a thread may append its own scattered ray and a new path)
-  if (fin) atomicAdd(&nfin, 1u);
-  __syncthreads();
-  if (threadIdx.x == 0 && nfin) base_k = atomicAdd(&w.cnt[16 + sh], nfin);
-  __syncthreads();
-  bool to_q2 = false;
-  PathState st;
-  if (threadIdx.x < nfin) {
-    const uint64_t P = a.n_paths;
-    uint64_t k = (uint64_t)base_k + threadIdx.x;
-    uint32_t ss = sh, tries = 0;
-    for (;;) {
-      const uint64_t id = k * WF_SHARDS + ss;
-      if (id >= P) {  // this dispenser is dry: the others may not be
-        if (++tries == WF_SHARDS) break;  // out of path ids everywhere
-        ss = (ss + 1u) & (WF_SHARDS - 1u);
-        k = atomicAdd(&w.cnt[16 + ss], 1u);
-        continue;
-      }
-      if (start_path<true>(start_lds[0], id, st)) {
-        to_q2 = true;
-        break;
-      }
-      k = atomicAdd(&w.cnt[16 + ss], 1u);  // an id off the image (a partial tile): draw another (rare)
-    }
-  }
-  // appends to the next queue: offsets from an LDS counter, one global atomic per block, one contiguous range
-  const uint32_t oq = to_q ? atomicAdd(&nap, 1u) : 0u, oq2 = to_q2 ? atomicAdd(&nap, 1u) : 0u;
-  __syncthreads();
-  if (threadIdx.x == 0 && nap) base_q = atomicAdd(&w.cnt[(1 - par) * 8 + sh], nap);
-  __syncthreads();
-  const WfQueue& O = w.q[1 - par];
-  const uint32_t ob = sh * w.shard_cap + base_q;
-  if (to_q) {
-    O.o_t[ob + oq] = o_t;
-    O.d_dep[ob + oq] = d_dep;
-    O.T_pid[ob + oq] = T_pid;
-    O.rng[ob + oq] = rg;
-  }
-  if (to_q2) {
-    O.o_t[ob + oq2] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.time);
-    O.d_dep[ob + oq2] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, __uint_as_float(st.depth));
-    O.T_pid[ob + oq2] = make_float4(1.f, 1.f, 1.f, __uint_as_float(st.pid));
-    O.rng[ob + oq2] = make_uint2((uint32_t)st.rng, (uint32_t)(st.rng >> 32));
-  }
-}
-
-__global__ void wf_init_kernel(WfArgs w) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 32) w.cnt[i] = 0u;
-}
+// The wavefront prototype (knob RTW_WAVEFRONT=1; measured slower, DESIGN.md §4 "Trace / shade split")
+#include "rtw_wavefront.inc"
 
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
                                     uint32_t n_tiles, const float* packed, float* img) {
