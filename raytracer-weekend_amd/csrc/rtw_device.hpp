@@ -123,6 +123,7 @@ enum ShadeMode : uint32_t {
   SM_GENERIC = 0,  // read mats[prim.mat] / texs[] (image, noise, uv-debug, nested checkers)
   SM_SOLID = 1,    // SolidColor: a = colour (texture.rs:56-60); Metal: a = albedo
   SM_CHECKER = 2,  // Checker(SolidColor odd, SolidColor even, freq): a = odd, b = even (texture.rs:69-81)
+  SM_IMAGE = 3,    // ImageTexture: a = (texel offset, width, height) as bits (image_texture.rs:34-52)
 };
 struct alignas(16) DevShade {
   uint32_t kind;  // bits 0..7 MatType, bits 8..11 ShadeMode, bit 12 the material reads uv

@@ -749,6 +749,10 @@ int flatten(Scene& s) {
         memcpy(d.a, f.texs[t.odd].c, sizeof d.a);
         memcpy(d.b, f.texs[t.even].c, sizeof d.b);
         d.param = t.freq;
+      } else if (t.type == TT_IMAGE) {  // the texel lookup needs no material / texture record loads
+        mode = SM_IMAGE;
+        const uint32_t img[3] = {t.off, t.w, t.h};
+        memcpy(d.a, img, sizeof d.a);
       }
     }
     d.kind = m.type | (mode << 8) | (m.needs_uv ? 1u << 12 : 0u);

@@ -1193,6 +1193,21 @@ __device__ __forceinline__ float perlin_turbulence(const DevPerlin& P, V3 p, int
   return fabsf(accum);
 }
 
+// image_texture.rs:34-52 over RGBX8 texels (rtw_flatten.cpp): one aligned 4-byte load
+__device__ __forceinline__ V3 image_texel(const DevScene& S, uint32_t off, uint32_t tw, uint32_t th, float u, float v) {
+  float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+  float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  float vv = 1.0f - vc;
+  float fi = uu * (float)tw, fj = vv * (float)th;
+  uint32_t i = (fi != fi || fi <= 0.0f) ? 0u : (fi >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fi);
+  uint32_t j = (fj != fj || fj <= 0.0f) ? 0u : (fj >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fj);
+  i = i > tw - 1 ? tw - 1 : i;
+  j = j > th - 1 ? th - 1 : j;
+  const uint32_t px = *reinterpret_cast<const uint32_t*>(S.texels + off + ((size_t)j * tw + i) * 4);
+  const float sc = 1.0f / 255.0f;
+  return mk((float)(px & 0xffu) * sc, (float)((px >> 8) & 0xffu) * sc, (float)((px >> 16) & 0xffu) * sc);
+}
+
 // ---- textures (texture.rs:56-81, :89-104; image_texture.rs:34-52)
 template <uint32_t FEAT>
 __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) {
@@ -1203,20 +1218,7 @@ __device__ V3 tex_value(const DevScene& S, uint32_t id, float u, float v, V3 p) 
       id = checker_odd(t.freq * p.x, t.freq * p.y, t.freq * p.z) ? t.odd : t.even;
       continue;
     }
-    if ((FEAT & F_IMAGE) && t.type == TT_IMAGE) {
-      float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
-      float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-      float vv = 1.0f - vc;
-      float fi = uu * (float)t.w, fj = vv * (float)t.h;
-      uint32_t i = (fi != fi || fi <= 0.0f) ? 0u : (fi >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fi);
-      uint32_t j = (fj != fj || fj <= 0.0f) ? 0u : (fj >= 4294967295.0f ? 0xFFFFFFFFu : (uint32_t)fj);
-      i = i > t.w - 1 ? t.w - 1 : i;
-      j = j > t.h - 1 ? t.h - 1 : j;
-      // image_texture.rs:34-52; texels are RGBX8 on the device (rtw_flatten.cpp): one 4-byte load
-      const uint32_t px = *reinterpret_cast<const uint32_t*>(S.texels + t.off + ((size_t)j * t.w + i) * 4);
-      const float sc = 1.0f / 255.0f;
-      return mk((float)(px & 0xffu) * sc, (float)((px >> 8) & 0xffu) * sc, (float)((px >> 16) & 0xffu) * sc);
-    }
+    if ((FEAT & F_IMAGE) && t.type == TT_IMAGE) return image_texel(S, t.off, t.w, t.h, u, v);
     if ((FEAT & F_NOISE) && t.type == TT_NOISE) {  // texture.rs:89-95
       const float tb = perlin_turbulence(S.perlins[t.off], p, 7);
       const float sv = 0.5f * (1.0f + dev_sinf(t.freq * p.z + 10.0f * tb));
@@ -1530,6 +1532,8 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         else if ((FEAT & F_CHECKER) && mode == SM_CHECKER)
           att = checker_odd(sh.param * h.p.x, sh.param * h.p.y, sh.param * h.p.z) ? ld3(sh.a)
                                                                                    : ld3(LST ? S.shade[b.prim].b : sh.b);
+        else if ((FEAT & F_IMAGE) && mode == SM_IMAGE)  // (the monument's texture: no record chain)
+          att = image_texel(S, __float_as_uint(sh.a[0]), __float_as_uint(sh.a[1]), __float_as_uint(sh.a[2]), h.u, h.v);
         else if (FEAT & F_TEXGEN) att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
       }
       if (light) {  // emit, no scatter
