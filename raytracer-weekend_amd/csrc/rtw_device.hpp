@@ -94,12 +94,7 @@ constexpr int MAX_INST_OPS = 6;
 struct alignas(16) DevInst {
   uint32_t nops, pad[3];
   float op[MAX_INST_OPS][4];  // (type, x, y, z) translate  |  (type, sin, cos, 0) rotate_y
-  // list-mode worlds: the padded object-space box of this chain's primitives, which are one contiguous run
-  // of box_lo[3] (bits) primitives in the always-tested list (0 = no run: never skipped).  A wave skips the
-  // run when no lane's object-space ray enters the box before its closest hit so far (culling only).
-  float box_lo[4], box_hi[4];
 };
-static_assert(sizeof(DevInst) == 144, "DevInst must be 144 B");
 
 enum MatType : uint32_t { MT_LAMBERT = 0, MT_METAL = 1, MT_DIELECTRIC = 2, MT_LIGHT = 3, MT_ISOTROPIC = 4 };
 struct alignas(16) DevMat {

@@ -61,7 +61,6 @@ void pad_box(Box& b) {
 struct Leaf {
   DevPrim p;
   Box wbox;
-  Box lbox;  // padded box in the space of the prim's innermost wrapper (DevInst::box_lo / box_hi)
   float c[3];
 };
 
@@ -131,8 +130,6 @@ struct Builder {
     Leaf L;
     L.p = p;
     L.wbox = to_world(local, box_chain ? *box_chain : chain);
-    L.lbox = local;
-    pad_box(L.lbox);
     for (int a = 0; a < 3; ++a) L.c[a] = 0.5f * (L.wbox.lo[a] + L.wbox.hi[a]);
     leaves.push_back(L);
   }
@@ -700,35 +697,6 @@ int flatten(Scene& s) {
   for (const Leaf& L : huge) {
     f.always.push_back((uint32_t)f.prims.size());
     f.prims.push_back(L.p);
-  }
-  // list mode: every wrapper chain whose primitives form ONE contiguous run of the always-tested list (a
-  // Cuboid's six rects) gets that run's length and padded object-space box (DevInst::box_lo / box_hi), so a
-  // wave can skip the run when no lane's ray enters the box.  Knob RTW_CHAIN_SKIP=0: off.
-  {
-    const char* knob = getenv("RTW_CHAIN_SKIP");
-    const bool on = (!knob || atoi(knob)) && rest.empty();
-    std::vector<uint32_t> runs(f.insts.size(), 0);
-    std::vector<Box> boxes(f.insts.size());
-    std::vector<uint8_t> bad(f.insts.size(), 0);
-    uint32_t prev = UINT32_MAX;
-    for (const Leaf& L : huge) {
-      const uint32_t i = L.p.type_inst >> 8;
-      if (i != prev && runs[i]) bad[i] = 1;  // a second run of the same chain
-      runs[i] += 1;
-      boxes[i].grow(L.lbox);
-      prev = i;
-    }
-    for (size_t i = 1; i < f.insts.size(); ++i) {
-      DevInst& in = f.insts[i];
-      const bool use = on && runs[i] >= 2 && !bad[i] && boxes[i].valid();
-      const uint32_t run = use ? runs[i] : 0u;
-      for (int a = 0; a < 3; ++a) {
-        in.box_lo[a] = use ? boxes[i].lo[a] : -INFINITY;
-        in.box_hi[a] = use ? boxes[i].hi[a] : INFINITY;
-      }
-      memcpy(&in.box_lo[3], &run, sizeof run);
-      in.box_hi[3] = 0.f;
-    }
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
   // triangle shading data re-indexed by prim (tshade[k] belongs to prims[k]): the winner's

@@ -715,27 +715,6 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
       if (inst != cur) {
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
         cur = inst;
-        if constexpr ((FEAT & F_LIST) != 0) {
-          // list mode: skip the chain's run of primitives (a Cuboid's six rects) when no lane's object-space
-          // ray enters its padded box before the closest hit so far (culling only, as the BVH's boxes)
-          if (inst) {
-            const float4 blo = uload(reinterpret_cast<const float4*>(S.insts[inst].box_lo));
-            const uint32_t run = __float_as_uint(blo.w);
-            if (run) {
-              const float4 bhi = uload(reinterpret_cast<const float4*>(S.insts[inst].box_hi));
-              auto safe_inv = [](float d) { return __builtin_amdgcn_rcpf(fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d)); };
-              const V3 inv = mk(safe_inv(lr.d.x), safe_inv(lr.d.y), safe_inv(lr.d.z));
-              const V3 ood = mk(lr.o.x * inv.x, lr.o.y * inv.y, lr.o.z * inv.z);
-              const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
-              float tn;
-              const bool in = slab_test(blo.x, blo.y, blo.z, bhi.x, bhi.y, bhi.z, inv, ood, tmax_c, tn);
-              if (!__any(in)) {
-                k += run - 1u;
-                continue;
-              }
-            }
-          }
-        }
       }
       test_prim<COUNT, FEAT, true, true>(S, pi, lr, ts.b, cnt, seg);
     }
