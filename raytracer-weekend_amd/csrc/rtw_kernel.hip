@@ -1393,25 +1393,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   __shared__ uint64_t pool_lds[BLK / 64][3];
   uint64_t* const pool = pool_lds[threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
-  // STG (list-mode kernels, whose LDS is nearly free): finished samples are staged per wave in LDS, one ring
-  // slot per group of 64 consecutive path ids (one tile-sample), and a complete group leaves as 768
-  // contiguous bytes in three 256-B wave stores -- instead of 64 separate 12-B stores that reach L2 at 64
-  // different times and leave it as partial lines (the sample stream's write amplification).
-  // A group is staged only if its first id claims a free slot (slot = group mod 4); otherwise its paths store
-  // directly.  Ids reach a wave in whole 1024-id pools, so a staged group's 64 paths all finish in this wave.
-  constexpr bool STG = (FEAT & F_LIST) != 0 && (FEAT & ~(F_BOXES | F_LIST)) == 0 && RTW_NT_SAMPLES;
-  constexpr int NSG = 4;
-  __shared__ float stage_all[STG ? BLK / 64 : 1][STG ? NSG * 192 : 1];
-  __shared__ uint32_t sgid_all[STG ? BLK / 64 : 1][NSG], scnt_all[STG ? BLK / 64 : 1][NSG];
-  float* const stage = stage_all[STG ? threadIdx.x >> 6 : 0];
-  uint32_t* const sgid = sgid_all[STG ? threadIdx.x >> 6 : 0];
-  uint32_t* const scnt = scnt_all[STG ? threadIdx.x >> 6 : 0];
-  if (STG && lane < (uint32_t)NSG) { sgid[lane] = ~0u; scnt[lane] = 0u; }
-  // a staged group's sample count (a finished path, or an id off the image); true for the 64th
-  auto stage_done = [&](uint32_t pid) -> bool {
-    const uint32_t s = (pid >> 6) & (NSG - 1);
-    return atomicAdd(&scnt[s], 1u) == 63u;
-  };
   bool exhausted = false;                // wave-uniform
   bool has = false;
   TraceState ts;
@@ -1434,21 +1415,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   };
   for (;;) {
     phase(2);
-    if constexpr (STG) {  // (every lane is here) complete groups leave as 768 contiguous bytes: 3 wave stores
-      uint64_t cm = __ballot(!has && (st.pid & 0x80000000u) != 0u);
-      while (cm) {
-        const int l = __ffsll((long long)cm) - 1;
-        cm &= cm - 1;
-        const uint32_t g = ((uint32_t)__shfl((int)st.pid, l, 64) & 0x7FFFFFFFu) >> 6, sl = g & (NSG - 1);
-        float* o = a.sbuf + (size_t)g * 192u;
-        const float* q = stage + sl * 192;
-        __builtin_nontemporal_store(q[lane], o + lane);
-        __builtin_nontemporal_store(q[64 + lane], o + 64 + lane);
-        __builtin_nontemporal_store(q[128 + lane], o + 128 + lane);
-        if (lane == 0) { sgid[sl] = ~0u; scnt[sl] = 0u; }
-      }
-      if (!has) st.pid &= 0x7FFFFFFFu;
-    }
     // ---- regeneration: compact new path ids into the idle lanes
     const uint64_t need = __ballot(!has);
     if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
@@ -1471,26 +1437,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         }
       }
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
-      if constexpr (STG) {
-        // groups whose first id is handed out now claim their ring slot if it is free (in lane order)
-        const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        uint64_t fm = __ballot(!has && (rank < avail || id < ne) && (id & 63u) == 0);
-        while (fm) {
-          const int l = __ffsll((long long)fm) - 1;
-          fm &= fm - 1;
-          const uint32_t g = (uint32_t)__shfl((int)(uint32_t)(id >> 6), l, 64);
-          const uint32_t sl = g & (NSG - 1);
-          if (lane == 0 && sgid[sl] == ~0u) { sgid[sl] = g; scnt[sl] = 0u; }
-        }
-      }
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, STACK>(SA, id, st, stk16)) {
-          has = true;
-        } else if (STG && (rank < avail || id < ne) && sgid[(uint32_t)(id >> 6) & (NSG - 1)] == (uint32_t)(id >> 6)) {
-          // an id off the image (a partial tile) counts toward its staged group; a 64th completes it (rare)
-          if (stage_done((uint32_t)id)) st.pid = (uint32_t)id | 0x80000000u;
-        }
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, STACK>(SA, id, st, stk16)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1628,18 +1577,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         } else {
           done = --st.depth == 0u;
         }
-      }
-    }
-    if (STG && done) {
-      const uint32_t pid = st.pid, g = pid >> 6, sl = g & (NSG - 1);
-      if (sgid[sl] == g) {
-        float* q = stage + sl * 192 + (pid & 63u) * 3u;
-        q[0] = L.x;
-        q[1] = L.y;
-        q[2] = L.z;
-        if (stage_done(pid)) st.pid = pid | 0x80000000u;  // this lane completed the group: flush below
-        has = false;
-        done = false;
       }
     }
     if (done) {
