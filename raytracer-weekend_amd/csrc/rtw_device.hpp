@@ -224,11 +224,6 @@ struct RenderArgs {
   int32_t* spill;                // traversal stack entries beyond the LDS stack: [depth][lane]
   uint32_t spill_depth;          // entries per lane (0 = the LDS stack covers the tree's bound)
   uint32_t spill_lanes;          // resident lanes of the launch (stride between levels)
-  // Tile-local id dispensing (knob RTW_WG_TILES): workgroup w first takes the batches of tile slots
-  // w, w + G, w + 2G, ... (G = the grid) from its own LDS counter, wg_rounds slots in all, each slot
-  // 2^wg_bps batches of `batch` ids; then ids from static_ids on come from the global queue.  0 = off.
-  uint32_t wg_rounds, wg_bps;
-  uint64_t static_ids;
 };
 
 }  // namespace rtw

@@ -1393,10 +1393,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   __shared__ uint64_t pool_lds[BLK / 64][3];
   uint64_t* const pool = pool_lds[threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
-  // RenderArgs::wg_rounds: this workgroup's next tile-local batch (its waves share the tile: L1 / L2 locality)
-  __shared__ uint32_t wg_next;
-  if (threadIdx.x == 0) wg_next = 0u;
-  __syncthreads();
   bool exhausted = false;                // wave-uniform
   bool has = false;
   TraceState ts;
@@ -1431,20 +1427,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       if (avail < n_need) {  // refill: one atomic per BATCH paths
         // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        if (lane == 0) {
-          uint64_t nbase = 0;
-          bool global = true;
-          if (a.wg_rounds) {  // tile-local batches first (RenderArgs::wg_rounds), then the global queue
-            const uint32_t k = atomicAdd(&wg_next, 1u);
-            if ((k >> a.wg_bps) < a.wg_rounds) {  // wg_bps = log2(batches per slot)
-              const uint32_t slot = blockIdx.x + gridDim.x * (k >> a.wg_bps);
-              nbase = (((uint64_t)slot << a.wg_bps) + (k & ((1u << a.wg_bps) - 1u))) * a.batch;
-              global = false;
-            }
-          }
-          if (global) nbase = a.static_ids + atomicAdd(a.queue, (unsigned long long)a.batch);
-          pool[2] = nbase;
-        }
+        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)a.batch);
         const uint64_t b = rfl64(pool[2]);
         if (b < P) {
           nb = b;
@@ -1506,7 +1489,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         // for every wave and empty this wave's id pool, so the grid drains after about one trip per wave
         // instead of one per 64 paths (a trip is 2^20 node-loop iterations)
         atomicMax(a.queue, (unsigned long long)P);
-        atomicMax(&wg_next, 0x7FFFFFFFu);
         pool[0] = pool[1];
       }
     } else {
@@ -2206,22 +2188,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     a.spill = c.spill;
     // the wavefront prototype (knob RTW_WAVEFRONT=1): the 1024-lane LDS-node sphere worlds, plain renders only
     const bool wavefront = env_int("RTW_WAVEFRONT", 0) == 1 && !count && var.k16 && var.block == 1024u;
-    // tile-local dispensing (RenderArgs::wg_rounds): RTW_WG_TILES percent of a pass's tile slots are dealt to
-    // the workgroups round-robin up front (each a whole tile at a time), the rest goes through the global queue
-    const int wg_pct = std::min(100, std::max(0, env_int("RTW_WG_TILES", 0)));
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
       a.n_paths = (uint64_t)ns * per_slot;
-      a.wg_rounds = 0;
-      a.wg_bps = 0;
-      a.static_ids = 0;
-      const uint64_t bps = per_slot / a.batch;
-      if (wg_pct && !wavefront && per_slot % a.batch == 0 && (bps & (bps - 1)) == 0) {
-        a.wg_rounds = (uint32_t)(((uint64_t)ns * (uint32_t)wg_pct / 100u) / (uint32_t)grid);
-        a.wg_bps = (uint32_t)__builtin_ctzll(bps);
-        a.static_ids = (uint64_t)a.wg_rounds * (uint32_t)grid * per_slot;
-      }
       if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
       hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
