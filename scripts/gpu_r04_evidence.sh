@@ -19,6 +19,12 @@ if [ -z "$NOTEST" ]; then
   timeout -k 10 300 python bench.py --config jumpy-400 --steps 5 --warmup 2 > gpurun_out/${TAG}bench_jumpy-400.log 2>&1 || { tail -5 gpurun_out/${TAG}bench_jumpy-400.log; exit 1; }
   timeout -k 10 300 python bench.py --multi-device 1 --steps 5 --warmup 2 --no-cpu-baseline \
     > gpurun_out/${TAG}multi_device1_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}multi_device1_bench.log; exit 1; }
+  # --gpus 2 without a launcher on a one-GPU box: must exit non-zero and print no bench line
+  if timeout -k 10 120 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/${TAG}gpus2_no_launcher.log 2>&1; then
+    echo "bench.py --gpus 2 succeeded on a one-GPU box"; exit 1
+  fi
+  grep -c '"n_gpus"' gpurun_out/${TAG}gpus2_no_launcher.log && { echo "a bench line was printed"; exit 1; }
+  tail -1 gpurun_out/${TAG}gpus2_no_launcher.log
 fi
 cd /tmp && export TMPDIR=/tmp
 for c in ${CONFIGS:-jumpy-1080p cornell-800 cow-1080p monument-4k}; do
