@@ -759,12 +759,14 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2_t as_h2(uint32_t u) { return __builtin_bit_cast(half2_t, u); }
 
-template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP, bool HN = false>
+// S16: the global-node walk keeps 16-bit stack entries (the nodes' 16-bit codes, sign-extended: leaves < 0)
+// in the uint16 column `stk16`, half the LDS of the 32-bit stack (RTW_MESH_S16: more workgroups per CU)
+template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP, bool HN = false, bool S16 = false>
 __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32_t* stk, int32_t* spill,
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
                           uint32_t* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
-  constexpr bool CODES = K16 || HN;  // leaves are 16-bit codes (the 32-bit walk keeps them sign-extended)
+  constexpr bool CODES = K16 || HN || S16;  // leaves are 16-bit codes (the 32-bit walk keeps them sign-extended)
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
   if constexpr (SPH_ONLY) rq = sph_rcp(r);
@@ -825,8 +827,12 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
         int32_t top = 0;
         if (can) {
           const int32_t i = ts.sp - 1;
-          top = stk[(SPILL ? min(i, STACK) : i) * BLK];
-          if (SPILL && i >= STACK) top = spill[(size_t)(i - STACK) * spill_lanes];  // rare
+          if constexpr (S16) {
+            top = (int32_t)(int16_t)stk16[i * BLK];
+          } else {
+            top = stk[(SPILL ? min(i, STACK) : i) * BLK];
+            if (SPILL && i >= STACK) top = spill[(size_t)(i - STACK) * spill_lanes];  // rare
+          }
         }
         const bool popn = can && top >= 0;
         const bool popl = can && top < 0 && ts.pend == 0;
@@ -897,7 +903,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           }
         } else {
           const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
-          constexpr uint32_t CWO = K16 ? 112u : 96u;    // child codes (K16) or child words
+          constexpr uint32_t CWO = (K16 || S16) ? 112u : 96u;  // child codes (K16, S16) or child words
           const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
           const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
           const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny));
@@ -909,7 +915,12 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           NX[0] = qnx.x; NX[1] = qnx.y; NX[2] = qnx.z; NX[3] = qnx.w; FX[0] = qfx.x; FX[1] = qfx.y; FX[2] = qfx.z; FX[3] = qfx.w;
           NY[0] = qny.x; NY[1] = qny.y; NY[2] = qny.z; NY[3] = qny.w; FY[0] = qfy.x; FY[1] = qfy.y; FY[2] = qfy.z; FY[3] = qfy.w;
           NZ[0] = qnz.x; NZ[1] = qnz.y; NZ[2] = qnz.z; NZ[3] = qnz.w; FZ[0] = qfz.x; FZ[1] = qfz.y; FZ[2] = qfz.z; FZ[3] = qfz.w;
-          CW[0] = cw.x; CW[1] = cw.y; CW[2] = cw.z; CW[3] = cw.w;
+          if constexpr (S16 && !K16) {  // 16-bit codes, sign-extended: internal >= 0, leaf < 0
+            CW[0] = (int32_t)(int16_t)cw.x; CW[1] = (int32_t)(int16_t)cw.y;
+            CW[2] = (int32_t)(int16_t)cw.z; CW[3] = (int32_t)(int16_t)cw.w;
+          } else {
+            CW[0] = cw.x; CW[1] = cw.y; CW[2] = cw.z; CW[3] = cw.w;
+          }
         }
         if (COUNT) {
           cnt[0]++;
@@ -983,8 +994,12 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
           // branch-free: a child that is not pushed is written where the next push (or nothing)
           // lands, i.e. at or above the final top, never below it.  Rows 0..STACK exist; with
           // SPILL, row STACK is scratch and entries from STACK up live in HBM (sp < stack_need).
-          stk[(SPILL ? min(sp, STACK) : sp) * BLK] = CW[k];
-          if (SPILL && pk && sp >= STACK) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // rare
+          if constexpr (S16) {
+            stk16[sp * BLK] = (uint16_t)CW[k];
+          } else {
+            stk[(SPILL ? min(sp, STACK) : sp) * BLK] = CW[k];
+            if (SPILL && pk && sp >= STACK) spill[(size_t)(sp - STACK) * spill_lanes] = CW[k];  // rare
+          }
           sp += pk ? 1 : 0;
         }
         ts.sp = sp;
@@ -1338,13 +1353,15 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
 
 // BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
-template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, bool HN = false>
+template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, bool HN = false,
+          bool S16 = false>
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void path_kernel(RenderArgs a) {
-  // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included)
-  __shared__ int32_t stk_all[NCAP > 0 ? 1 : (STACK + 1) * BLK];
+  // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included);
+  // S16 (global nodes, 16-bit entries): STACK + 1 rows of 16 bits
+  __shared__ int32_t stk_all[(NCAP > 0 || S16) ? 1 : (STACK + 1) * BLK];
   // LST: 10 more 16-bit rows after the stack hold the path state (below)
   constexpr int LST_ROWS = (NCAP > 0 && BLK == 1024) ? 10 : 0;
-  __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : 1];
+  __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1) * BLK : 1)];
   constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
@@ -1466,7 +1483,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
-      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP, HN>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
+      trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP, HN, S16>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
                                                       leaf_thr, st.rng, a.err, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
@@ -1865,8 +1882,15 @@ constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
 // (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
 // from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
 template <bool C, uint32_t F>
-static Variant pick5(uint32_t need, bool half = false) {
+static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
   using namespace dev;
+  if constexpr (F == F_MESHES) {
+    // RTW_MESH_S16 = 6: 16-bit stack entries (half the LDS) at 6 waves / SIMD (the 32-bit stack's 31 KB per
+    // workgroup allows 5 per CU)
+    if (codes16 && env_int("RTW_MESH_S16", 0) == 6 && need <= (uint32_t)STACK_DEEP5)
+      return half ? Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, (uint32_t)STACK_DEEP5}
+                  : Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, (uint32_t)STACK_DEEP5};
+  }
   if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built
     if (half && need <= (uint32_t)STACK_LDS5)
       return {path_kernel<C, STACK_LDS5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_LDS5};
@@ -1953,7 +1977,7 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
         // a partial LDS node cache (the top 128 / 376 / 760 node4s, the rest from global memory, sorted-push
         // walk) measured slower on cow / monument (profiles/r02/experiments, n7): the full-table kernels
         // are for trees that fit
-        return pick5<C, F_MESHES>(need, half);
+        return pick5<C, F_MESHES>(need, half, codes16);
       }
       return pick5<C, F_ALL>(need);
   }
