@@ -1885,11 +1885,20 @@ template <bool C, uint32_t F>
 static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
   using namespace dev;
   if constexpr (F == F_MESHES) {
-    // RTW_MESH_S16 = 6: 16-bit stack entries (half the LDS) at 6 waves / SIMD (the 32-bit stack's 31 KB per
-    // workgroup allows 5 per CU)
-    if (codes16 && env_int("RTW_MESH_S16", 0) == 6 && need <= (uint32_t)STACK_DEEP5)
-      return half ? Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, (uint32_t)STACK_DEEP5}
-                  : Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, (uint32_t)STACK_DEEP5};
+    // 16-bit stack entries (the nodes' codes: half the LDS of the 32-bit stack, whose 31 KB per workgroup allow
+    // 5 per CU) at 6, 7 or 8 waves / SIMD (knob RTW_MESH_S16; 0 = the 32-bit stack at 5).  Measured (r04n):
+    // monument-4k +3.0% at 6 waves (80 VGPRs, 40 B scratch), cow-1080p -4.1%, so by default the half-node
+    // trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
+    const int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
+    if (codes16 && s16 >= 6 && need <= (uint32_t)STACK_DEEP5) {
+      const uint32_t st = (uint32_t)STACK_DEEP5;
+      if (half) {
+        if (s16 == 7) return {path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st};
+        if (s16 == 8) return {path_kernel<C, STACK_DEEP5, false, 8, F, BLOCK, 0, true, true>, st};
+        return {path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, st};
+      }
+      return {path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, st};
+    }
   }
   if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built
     if (half && need <= (uint32_t)STACK_LDS5)
