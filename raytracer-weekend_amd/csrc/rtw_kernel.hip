@@ -1360,8 +1360,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // S16 (global nodes, 16-bit entries): STACK + 1 rows of 16 bits
   __shared__ int32_t stk_all[(NCAP > 0 || S16) ? 1 : (STACK + 1) * BLK];
   // LST: 10 more 16-bit rows after the stack hold the path state (below)
-  constexpr int LST_ROWS = (NCAP > 0 && BLK == 1024) ? 10 : 0;
-  __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1) * BLK : 1)];
+  // (the S16 mesh walk too: its 16-bit stack column has STACK + 1 rows, the state rows follow them)
+  constexpr int LST_ROWS = ((NCAP > 0 && BLK == 1024) || S16) ? 10 : 0;
+  constexpr int LST_ROW0 = STACK + (S16 ? 1 : 0);
+  __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1 + LST_ROWS) * BLK : 1)];
   constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
@@ -1394,11 +1396,11 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // loop-invariant VGPRs, which the compiler spilled in turn.
   constexpr bool LST = LST_ROWS > 0;
   auto lst_st = [&](int k, uint32_t v) {
-    stk16[(STACK + 2 * k) * BLK] = (uint16_t)v;
-    stk16[(STACK + 2 * k + 1) * BLK] = (uint16_t)(v >> 16);
+    stk16[(LST_ROW0 + 2 * k) * BLK] = (uint16_t)v;
+    stk16[(LST_ROW0 + 2 * k + 1) * BLK] = (uint16_t)(v >> 16);
   };
   auto lst_ld = [&](int k) -> uint32_t {
-    return (uint32_t)stk16[(STACK + 2 * k) * BLK] | ((uint32_t)stk16[(STACK + 2 * k + 1) * BLK] << 16);
+    return (uint32_t)stk16[(LST_ROW0 + 2 * k) * BLK] | ((uint32_t)stk16[(LST_ROW0 + 2 * k + 1) * BLK] << 16);
   };
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
@@ -1456,7 +1458,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, STACK>(SA, id, st, stk16)) has = true;
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0>(SA, id, st, stk16)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
