@@ -1888,18 +1888,18 @@ static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
   using namespace dev;
   if constexpr (F == F_MESHES) {
     // 16-bit stack entries (the nodes' codes: half the LDS of the 32-bit stack, whose 31 KB per workgroup allow
-    // 5 per CU) at 6, 7 or 8 waves / SIMD (knob RTW_MESH_S16; 0 = the 32-bit stack at 5).  Measured (r04n):
-    // monument-4k +3.0% at 6 waves (80 VGPRs, 40 B scratch), cow-1080p -4.1%, so by default the half-node
-    // trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
+    // 5 per CU) and the paths' T / depth / id in LDS state rows, at 6 or 7 waves / SIMD (knob RTW_MESH_S16; 0 =
+    // the 32-bit stack at 5).  Measured (r04n, r04p): monument-4k +3.0% at 6 waves (80 VGPRs), +2.2% more with
+    // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows, so by default
+    // the half-node trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
     const int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
     if (codes16 && s16 >= 6 && need <= (uint32_t)STACK_DEEP5) {
       const uint32_t st = (uint32_t)STACK_DEEP5;
-      if (half) {
-        if (s16 == 7) return {path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st};
-        if (s16 == 8) return {path_kernel<C, STACK_DEEP5, false, 8, F, BLOCK, 0, true, true>, st};
-        return {path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, st};
-      }
-      return {path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, st};
+      if (s16 == 7)
+        return half ? Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st}
+                    : Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, false, true>, st};
+      return half ? Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, st}
+                  : Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, st};
     }
   }
   if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built

@@ -117,7 +117,7 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
                                   "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5", "RTW_HALF_NODES=1",
                                   "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7",
                                   "RTW_LDSN_BLK=512", "RTW_MESH_S16=0", "RTW_MESH_S16=6",
-                                  "RTW_MESH_S16=7", "RTW_MESH_S16=8"])
+                                  "RTW_MESH_S16=7"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
