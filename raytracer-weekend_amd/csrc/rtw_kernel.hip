@@ -1924,11 +1924,13 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
   // Half-precision nodes (DevNode4h, built when the 16-bit codes fit) trade vector-memory traffic (4 loads /
   // 64 B per visit instead of 7 / 112 B) for VALU issue (v_fma_mix_f32 issues ~1.3x slower than v_fma_f32,
   // scripts/ubench/mix_rate.hip; +5 VALU per visit).  Measured (profiles/r03/experiments, h1): monument-4k
-  // +3.3% (its 2,226-node tree), cow-1080p -6.5% (1,591 nodes), jumpy-1080p -4.9% (LDS nodes).  So by
-  // default only mesh trees of >= 2048 node4s use them; knob RTW_HALF_NODES 1 = wherever built, 0 = never.
+  // +3.3% (its 2,226-node tree), cow-1080p -6.5% (1,591 nodes), jumpy-1080p -4.9% (LDS nodes) at round 3's 5-wave
+  // mesh kernel.  With round 4's 6-wave mesh walk (16-bit stack, LDS state rows; pick5) the cow gains too (r04q:
+  // +1.8%), so every mesh tree with a half table uses it by default; the LDS-node sphere kernels keep f32 nodes.
+  // Knob RTW_HALF_NODES 1 = wherever built (LDS-node kernels too), 0 = never.
   const int half_knob = env_int("RTW_HALF_NODES", -1);
   // (no half-precision table when a bound is beyond f16's range: rtw_flatten.cpp half_node)
-  const bool half = has_half && (half_knob > 0 || (half_knob < 0 && n_nodes >= 2048));
+  const bool half = has_half && half_knob != 0;
   const bool half_lds = has_half && half_knob > 0;
   if (list && !env_int("RTW_GENERIC", 0)) {
     // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
