@@ -324,7 +324,9 @@ struct BuildParams {
   int leaf_max = 4;
   float trav = 0.5f;
   int bins = 16;
+  uint32_t pair = 2;  // ranges of at most this many prims become leaves without a SAH decision
   BuildParams() {
+    if (const char* e = getenv("RTW_BVH_PAIR")) pair = (uint32_t)std::min(4, std::max(1, atoi(e)));
     if (const char* e = getenv("RTW_BVH_LEAF")) leaf_max = std::min(7, std::max(1, atoi(e)));
     if (const char* e = getenv("RTW_BVH_TRAV")) trav = (float)atof(e);
     if (const char* e = getenv("RTW_BVH_BINS")) bins = std::min(64, std::max(4, atoi(e)));
@@ -351,7 +353,7 @@ struct BvhBuild {
     for (uint32_t k = b; k < e; ++k) { box.grow(L[k].wbox); cbox.grow(L[k].c); }
     uint32_t n = e - b;
     if (depth > max_depth) max_depth = depth;
-    if (n <= 2) return Ref{box, (int32_t)b, n};
+    if (n <= P.pair) return Ref{box, (int32_t)b, n};
 
     // choose split
     int best_axis = -1;
