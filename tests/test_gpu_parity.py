@@ -117,18 +117,19 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
                                   "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5", "RTW_HALF_NODES=1",
                                   "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7",
                                   "RTW_LDSN_BLK=512", "RTW_MESH_S16=0", "RTW_MESH_S16=6",
-                                  "RTW_MESH_S16=7"])
+                                  "RTW_MESH_S16=7", "RTW_BVH_PAIR=1", "RTW_BVH_BINS=64"])
 def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
     operations are keyed by its (pixel, sample) id, so the image and the ray count must not move.
     Same for the node table in LDS vs global memory (RTW_LDS_NODES) and the occupancy variants
-    (RTW_OCC).  Same for list mode vs BVH (RTW_LIST_MAX): closest hit with ties to the later object is a
-    commutative reduction over the leaves, whatever culls them."""
+    (RTW_OCC).  Same for list mode vs BVH (RTW_LIST_MAX) and for other trees over the same prims (RTW_BVH_PAIR,
+    RTW_BVH_BINS): closest hit with ties to the later object is a commutative reduction over the leaves,
+    whatever culls them."""
     k, v = knob.split("=")
     monkeypatch.setenv(k, v)
     # the half-node knobs matter for BVH worlds: jumpy-balls (LDS nodes) and the cow (global nodes)
-    mesh = "HALF" in k or "TRI" in k or "MESH" in k
+    mesh = "HALF" in k or "TRI" in k or "MESH" in k or "BVH" in k
     for name, aspect, w, h, spp in ((SCENES[0], SCENES[2], SCENES[3]) if mesh else (SCENES[0], SCENES[1])):
         g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
         assert st["rays"] == rays
@@ -369,7 +370,7 @@ def _sphere_world(rtw, seed, n=120):
 
 
 @pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7", "RTW_HALF_NODES=1",
-                                  "RTW_LDSN_BLK=512"])
+                                  "RTW_LDSN_BLK=512", "RTW_BVH_PAIR=1"])
 @pytest.mark.parametrize("seed,n", [(1, 120), (2, 120), (3, 700)])
 def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
     """Sphere worlds run the LDS-node kernel (node table in LDS, sorted-push walk over 16-bit codes)
