@@ -253,3 +253,26 @@ def test_half_nodes_beyond_f16_range(rtw, offset, built):
             full = ~(nd["lo_x"] > nd["hi_x"])
             with np.errstate(invalid="ignore"):
                 assert np.all((org[:, None] + lo16 <= nd["lo_" + ax])[full]), ax
+
+
+@pytest.mark.parametrize("knob", ["RTW_BVH_PAIR=1", "RTW_BVH_PAIR=3", "RTW_BVH_BINS=64", "RTW_BVH_LEAF=2"])
+def test_bvh_build_knobs_cover_every_prim(rtw, monkeypatch, knob):
+    """The SAH build knobs (RTW_BVH_PAIR / BINS / LEAF) only reshape the tree: the flattener's own
+    self-check (every node4 reached once, every BVH prim in exactly one leaf) passes, the leaves' prim ranges
+    cover the BVH part once, and the 16-bit codes still hold (leaves of <= 4 prims)."""
+    k, v = knob.split("=")
+    monkeypatch.setenv(k, v)
+    for name in ("jumpy-balls", "wavefront-cow-obj"):
+        s = rtw.Scene()
+        s.preset(name, 16 / 9, seed=42)
+        _commit_anywhere(rtw, s)
+        nd = s.nodes()
+        assert len(nd) == s.info(3) > 4
+        full = ~(nd["lo_x"] > nd["hi_x"])
+        leaf = full & ((nd["code"] & 0x8000) != 0)
+        first, cnt = (nd["code"][leaf] >> 2) & 0x1FFF, (nd["code"][leaf] & 3) + 1
+        cover = np.zeros(int((first + cnt).max()), np.int32)
+        for f, c in zip(first, cnt):
+            cover[f:f + c] += 1
+        assert np.all(cover == 1), name
+        assert s.info(11) >= 4
