@@ -762,13 +762,6 @@ __device__ __forceinline__ half2_t as_h2(uint32_t u) { return __builtin_bit_cast
 // The LDS-node kernels with the 144-node f32 table hold it as DevNode4t (time-split planes on one axis; the
 // 224-node and half-precision forms have no LDS to spare and keep DevNode4 / DevNode4h)
 __host__ __device__ constexpr bool ts_table(int ncap, bool hn) { return ncap == 144 && !hn; }
-// the quad after the DevNode4t table in LDS: the byte offsets of the x / y / z planes for a ray in the second half
-// of the shutter (128 on the split axis, the DevNode4 offsets elsewhere) and time_mid's bits
-__device__ __forceinline__ void ts_quad(const DevScene& S, float4* q) {
-  const uint32_t ax = S.ts_axis;
-  *reinterpret_cast<uint4*>(q) = make_uint4(ax == 0u ? 128u : 0u, ax == 1u ? 128u : 32u, ax == 2u ? 128u : 64u,
-                                            __float_as_uint(S.time_mid));
-}
 
 // S16: the global-node walk keeps 16-bit stack entries (the nodes' 16-bit codes, sign-extended: leaves < 0)
 // in the uint16 column `stk16`, half the LDS of the 32-bit stack (RTW_MESH_S16: more workgroups per CU)
@@ -814,15 +807,13 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   // near / far plane byte offsets inside DevNode4 by the ray's direction signs (32-bit offsets
   // from the uniform table base: the loads take the SGPR-base + VGPR-offset form)
   uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
-  if constexpr (TS) {
-    // DevNode4t: a ray in the shutter's second half reads the split axis's planes at byte 128.  The per-axis
-    // plane bases of that half and time_mid sit in LDS after the table (ts_quad): as kernel arguments they
-    // cost SGPRs, which the LDS-node kernel spills to VGPR lanes (experiments e2 / e3)
-    const uint4 tq = *reinterpret_cast<const uint4*>(lnodes + NCAP * 10);
-    const bool h1 = r.time >= __uint_as_float(tq.w);
-    nx = (nx & 16u) + (h1 ? tq.x : 0u);
-    ny = (ny & 16u) + (h1 ? tq.y : 32u);
-    nz = (nz & 16u) + (h1 ? tq.z : 64u);
+  if constexpr (TS) {  // DevNode4t: a ray in the shutter's second half reads the split axis's planes at 128
+    if (r.time >= S.time_mid) {
+      const uint32_t ax = S.ts_axis;
+      nx = ax == 0u ? nx + 128u : nx;
+      ny = ax == 1u ? ny + 96u : ny;
+      nz = ax == 2u ? nz + 64u : nz;
+    }
   }
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
   const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes)
@@ -1389,13 +1380,12 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1 + LST_ROWS) * BLK : 1)];
   constexpr bool TS = ts_table(NCAP, HN);
   constexpr uint32_t NODE_Q = HN ? 7u : (TS ? 10u : 8u);  // 16-B quads per node (DevNode4h / DevNode4t / DevNode4)
-  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q + (TS ? 1 : 0) : 1];
+  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
     const float4* g = HN   ? reinterpret_cast<const float4*>(a.scene.hnodes)
                       : TS ? reinterpret_cast<const float4*>(a.scene.tnodes)
                            : reinterpret_cast<const float4*>(a.scene.nodes);
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * NODE_Q; k += BLK) nodes_lds[k] = g[k];
-    if (TS && threadIdx.x == 0) ts_quad(a.scene, nodes_lds + NCAP * NODE_Q);
   }
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
   // reload a v_readlane: cornell-800 +6%, jumpy +0.8%); the mesh variants regenerate paths every ~2
