@@ -82,19 +82,6 @@ struct alignas(16) DevNode4h {
 };
 static_assert(sizeof(DevNode4h) == 112, "DevNode4h must be 112 B");
 
-// The LDS-node kernels' table (built when Flat::codes16): a DevNode4 whose planes on ONE axis (DevScene::ts_axis,
-// the axis the moving spheres travel along most) bound the children over the first half of the shutter,
-// [time_lo, time_mid], followed by the same axis's planes over the second half, [time_mid, time_hi].  A ray
-// whose time is >= time_mid reads its near / far planes on that axis from `alt` (a different per-ray byte
-// offset, no work per visit), so each ray culls against boxes swept over half the motion (jumpy-balls: node
-// visits -6%, moving-sphere tests -16%, profiles/r04/experiments e1).  Both halves contain every position
-// the kernel's f32 center_at can produce in them (it is monotone in t), padded like every box.
-struct alignas(16) DevNode4t {
-  DevNode4 n;
-  float alt_lo[4], alt_hi[4];
-};
-static_assert(sizeof(DevNode4t) == 160, "DevNode4t must be 160 B");
-
 struct alignas(16) DevTriShade {
   float n[9];   // vertex normals after defaults (triangular.rs:55)
   float uv[6];  // vertex uvs after defaults (triangular.rs:57-66)
@@ -185,7 +172,6 @@ constexpr uint32_t F_MESHES = F_SPHERE | F_RECT | F_TRI | F_INST | F_CHECKER | F
 struct DevScene {
   const DevNode4* nodes;
   const DevNode4h* hnodes;  // the half-precision copy (nullptr unless Flat::codes16)
-  const DevNode4t* tnodes;  // the time-split copy for the LDS-node kernels (nullptr unless Flat::codes16)
   const DevPrim* prims;
   const uint32_t* always;
   const DevTriShade* tshade;
@@ -199,10 +185,9 @@ struct DevScene {
   uint32_t msphere_unit;  // every moving sphere's shutter is [+0, 1]: center_at needs no q2 / division
   uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
   float uni_off[3];
-  float time_mid;         // DevNode4t: rays with time >= time_mid read the second half's planes
+  uint32_t reserved0;     // (was rect_k_small, round 3's dropped reciprocal rect test; keeps the kernarg layout)
   uint32_t bvh_tri;       // every BVH leaf primitive is a triangle of instance tri_inst (the leaf fast path)
   uint32_t tri_inst;
-  uint32_t ts_axis;       // DevNode4t's split axis (0 x, 1 y, 2 z)
 };
 
 struct DevCamera {

@@ -18,8 +18,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <array>
-#include <functional>
 #include <map>
 #include <vector>
 
@@ -63,7 +61,6 @@ void pad_box(Box& b) {
 struct Leaf {
   DevPrim p;
   Box wbox;
-  Box hb[2];  // the world box over [time_lo, time_mid] and [time_mid, time_hi] (= wbox unless the prim moves)
   float c[3];
 };
 
@@ -133,7 +130,6 @@ struct Builder {
     Leaf L;
     L.p = p;
     L.wbox = to_world(local, box_chain ? *box_chain : chain);
-    L.hb[0] = L.hb[1] = L.wbox;
     for (int a = 0; a < 3; ++a) L.c[a] = 0.5f * (L.wbox.lo[a] + L.wbox.hi[a]);
     leaves.push_back(L);
   }
@@ -218,22 +214,16 @@ struct Builder {
         p.aux = (t0_bits == 0u && n.f[7] == 1.0f) ? 1u : 0u;
         p.mat = n.mat;
         float r = fabsf(n.f[8]);
-        // center_at_time (spherical.rs:117-123) is linear in t, and the kernel's f32 evaluation
-        // c0 + RN(frac * (c1 - c0)) is monotone in t: an interval's end points bound it.  The kernel
-        // refuses cameras outside [time_lo, time_hi]; the halves split at time_mid (DevNode4t).
-        auto swept = [&](float t0, float t1) {
-          Box b;
-          for (float t : {t0, t1}) {
-            float c[3];
-            for (int a = 0; a < 3; ++a) c[a] = n.f[a] + ((t - n.f[3]) / (n.f[7] - n.f[3])) * (n.f[4 + a] - n.f[a]);
-            float lo[3] = {c[0] - r, c[1] - r, c[2] - r}, hi[3] = {c[0] + r, c[1] + r, c[2] + r};
-            b.grow(lo); b.grow(hi);
-          }
-          return b;
-        };
-        emit(p, swept(f.time_lo, f.time_hi), chain);
-        leaves.back().hb[0] = to_world(swept(f.time_lo, f.time_mid), chain);
-        leaves.back().hb[1] = to_world(swept(f.time_mid, f.time_hi), chain);
+        Box b;
+        // center_at_time (spherical.rs:117-123) is linear in t: the shutter interval's end
+        // points bound it.  The kernel refuses cameras outside [time_lo, time_hi].
+        for (float t : {f.time_lo, f.time_hi}) {
+          float c[3];
+          for (int a = 0; a < 3; ++a) c[a] = n.f[a] + ((t - n.f[3]) / (n.f[7] - n.f[3])) * (n.f[4 + a] - n.f[a]);
+          float lo[3] = {c[0] - r, c[1] - r, c[2] - r}, hi[3] = {c[0] + r, c[1] + r, c[2] + r};
+          b.grow(lo); b.grow(hi);
+        }
+        emit(p, b, chain);
         return;
       }
       case NK_RECT:
@@ -439,23 +429,16 @@ struct BvhBuild {
 // Each 4-wide node absorbs up to two BVH2 levels: starting from a BVH2 node's two children, the
 // internal child with the largest surface area is repeatedly replaced by its own two children
 // until there are four.  Leaves keep their prim ranges (leaf word ~(first << 3 | count)).
-struct HalfBoxes {
-  Box hb[4][2];  // per node4 child: the box over each half of the shutter (DevNode4t)
-};
 struct Collapse {
   const std::vector<DevNode>& n2;
   std::vector<DevNode4>& out;
-  const std::vector<Leaf>& L;                   // BVH prims in leaf order
-  const std::vector<std::array<Box, 2>>& H;    // per BVH2 node: its subtree's half-shutter boxes
-  std::vector<HalfBoxes>& outh;                 // per node4, alongside `out`
 
   struct C {
     Box box;
-    Box hb[2];
     int32_t idx;     // BVH2 node (internal) or first prim (leaf)
     uint32_t count;  // 0 = internal
   };
-  C child(const DevNode& n, int k) const {
+  static C child(const DevNode& n, int k) {
     C c;
     for (int a = 0; a < 3; ++a) {
       c.box.lo[a] = k ? n.b1lo[a] : n.b0lo[a];
@@ -463,13 +446,6 @@ struct Collapse {
     }
     c.idx = k ? n.c1 : n.c0;
     c.count = k ? n.n1 : n.n0;
-    for (int h = 0; h < 2; ++h) {
-      c.hb[h] = Box();
-      if (c.count)
-        for (uint32_t q = 0; q < c.count; ++q) c.hb[h].grow(L[(size_t)c.idx + q].hb[h]);
-      else if (c.idx >= 0)
-        c.hb[h] = H[c.idx][h];
-    }
     return c;
   }
   // returns the node4 index; *bound = worst-case stack entries pushed below (and at) this node
@@ -500,7 +476,6 @@ struct Collapse {
       nd.hi_x[k] = nd.hi_y[k] = nd.hi_z[k] = -INFINITY;
     }
     out.push_back(nd);
-    outh.push_back(HalfBoxes{});
     uint32_t below = 0, below4 = 0;
     bool inner = false;
     for (size_t k = 0; k < ch.size(); ++k) {
@@ -519,8 +494,6 @@ struct Collapse {
       o.lo_y[k] = ch[k].box.lo[1]; o.hi_y[k] = ch[k].box.hi[1];
       o.lo_z[k] = ch[k].box.lo[2]; o.hi_z[k] = ch[k].box.hi[2];
       o.child[k] = word;
-      outh[id].hb[k][0] = ch[k].hb[0];
-      outh[id].hb[k][1] = ch[k].hb[1];
     }
     // a visit pushes every hit child except the nearest internal one, which it walks into next
     // (trace_run); with no internal child it may push them all
@@ -602,7 +575,6 @@ bool texture_reads_uv(const Scene& s, uint32_t t, int guard = 0) {
 int flatten(Scene& s) {
   Flat& f = s.flat;
   f = Flat();
-  f.time_mid = 0.5f * (f.time_lo + f.time_hi);
   // tables
   for (const MatH& m : s.mat) {
     DevMat d;
@@ -792,32 +764,7 @@ int flatten(Scene& s) {
   // 4-wide tree for the kernel
   if (!f.nodes.empty()) {
     if (rest.size() >= (1u << 28)) return fail(RTW_EINVAL, "too many BVH primitives for leaf words");
-    // per BVH2 node: its subtree's boxes over the two halves of the shutter (DevNode4t)
-    std::vector<std::array<Box, 2>> H(f.nodes.size());
-    {
-      auto leafbox = [&](int32_t first, uint32_t cnt, int h) {
-        Box b;
-        for (uint32_t q = 0; q < cnt; ++q) b.grow(rest[(size_t)first + q].hb[h]);
-        return b;
-      };
-      std::function<void(int32_t)> fill = [&](int32_t n) {
-        const DevNode& d = f.nodes[n];
-        for (int h = 0; h < 2; ++h) H[n][h] = Box();
-        for (int k = 0; k < 2; ++k) {
-          const int32_t c = k ? d.c1 : d.c0;
-          const uint32_t cnt = k ? d.n1 : d.n0;
-          if (cnt) {
-            for (int h = 0; h < 2; ++h) H[n][h].grow(leafbox(c, cnt, h));
-          } else if (c >= 0) {
-            fill(c);
-            for (int h = 0; h < 2; ++h) H[n][h].grow(H[c][h]);
-          }
-        }
-      };
-      fill(0);
-    }
-    std::vector<HalfBoxes> half4;
-    Collapse col{f.nodes, f.nodes4, rest, H, half4};
+    Collapse col{f.nodes, f.nodes4};
     uint32_t bound = 0, bound4 = 0;
     col.build(0, &bound, &bound4);
     f.stack_need4 = bound4;
@@ -862,15 +809,12 @@ int flatten(Scene& s) {
         }
       }
       std::vector<DevNode4> bfs(order.size());
-      std::vector<HalfBoxes> bfsh(order.size());
       for (size_t q = 0; q < order.size(); ++q) {
         bfs[q] = f.nodes4[order[q]];
-        bfsh[q] = half4[order[q]];
         for (int k = 0; k < 4; ++k)
           if (bfs[q].lo_x[k] <= bfs[q].hi_x[k] && bfs[q].child[k] >= 0) bfs[q].child[k] = renum[bfs[q].child[k]];
       }
       f.nodes4.swap(bfs);
-      half4.swap(bfsh);
     }
     // 16-bit child codes of the sorted-push walk (DevNode4::code): possible when node4 indices fit
     // 15 bits and every leaf has <= 4 prims starting below 8192
@@ -889,41 +833,6 @@ int flatten(Scene& s) {
         }
       }
     if (f.codes16) {
-      // DevNode4t: split the axis along which the half-shutter boxes shrink the most (summed extents; the
-      // moving balls of jumpy-balls travel in y).  Without motion both halves equal the full boxes.
-      double gain[3] = {0, 0, 0};
-      for (size_t q = 0; q < f.nodes4.size(); ++q)
-        for (int k = 0; k < 4; ++k) {
-          if (f.nodes4[q].lo_x[k] > f.nodes4[q].hi_x[k]) continue;
-          const float* lo[3] = {f.nodes4[q].lo_x, f.nodes4[q].lo_y, f.nodes4[q].lo_z};
-          const float* hi[3] = {f.nodes4[q].hi_x, f.nodes4[q].hi_y, f.nodes4[q].hi_z};
-          for (int a = 0; a < 3; ++a) {
-            const Box* hb = half4[q].hb[k];
-            gain[a] += 2.0 * ((double)hi[a][k] - lo[a][k]) - ((double)hb[0].hi[a] - hb[0].lo[a]) -
-                       ((double)hb[1].hi[a] - hb[1].lo[a]);
-          }
-        }
-      f.ts_axis = gain[0] > gain[1] && gain[0] > gain[2] ? 0u : (gain[2] > gain[1] ? 2u : 1u);
-      const int ax = (int)f.ts_axis;
-      f.nodes4t.resize(f.nodes4.size());
-      for (size_t q = 0; q < f.nodes4.size(); ++q) {
-        DevNode4t& t = f.nodes4t[q];
-        t.n = f.nodes4[q];
-        float* lo = ax == 0 ? t.n.lo_x : (ax == 1 ? t.n.lo_y : t.n.lo_z);
-        float* hi = ax == 0 ? t.n.hi_x : (ax == 1 ? t.n.hi_y : t.n.hi_z);
-        for (int k = 0; k < 4; ++k) {
-          t.alt_lo[k] = lo[k];
-          t.alt_hi[k] = hi[k];
-          if (lo[k] > hi[k]) continue;  // empty slot: inverted in both halves
-          const Box* hb = half4[q].hb[k];
-          // each half's box lies inside the full one (both unions of the same padded pieces); min / max
-          // keep it so even if a half were empty
-          lo[k] = std::max(lo[k], hb[0].lo[ax]);
-          hi[k] = std::min(hi[k], hb[0].hi[ax]);
-          t.alt_lo[k] = std::max(t.alt_lo[k], hb[1].lo[ax]);
-          t.alt_hi[k] = std::min(t.alt_hi[k], hb[1].hi[ax]);
-        }
-      }
       f.nodes4h.resize(f.nodes4.size());
       for (size_t q = 0; q < f.nodes4.size(); ++q)
         if (!half_node(f.nodes4[q], f.nodes4h[q])) {  // bounds beyond f16: the f32 table only

@@ -759,10 +759,6 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2_t as_h2(uint32_t u) { return __builtin_bit_cast(half2_t, u); }
 
-// The LDS-node kernels with the 144-node f32 table hold it as DevNode4t (time-split planes on one axis; the
-// 224-node and half-precision forms have no LDS to spare and keep DevNode4 / DevNode4h)
-__host__ __device__ constexpr bool ts_table(int ncap, bool hn) { return ncap == 144 && !hn; }
-
 // S16: the global-node walk keeps 16-bit stack entries (the nodes' 16-bit codes, sign-extended: leaves < 0)
 // in the uint16 column `stk16`, half the LDS of the 32-bit stack (RTW_MESH_S16: more workgroups per CU)
 template <bool COUNT, int STACK, bool SPILL, uint32_t FEAT, int BLK, int NCAP, bool HN = false, bool S16 = false>
@@ -770,7 +766,6 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
                           uint32_t spill_lanes, uint32_t* cnt, uint32_t quota, uint32_t leaf_thr, uint64_t seg,
                           uint32_t* err, uint64_t* tph, const float4* lnodes, uint16_t* stk16) {
   constexpr bool K16 = NCAP > 0;
-  constexpr bool TS = ts_table(NCAP, HN);  // the LDS table is DevNode4t (160 B per node)
   constexpr bool CODES = K16 || HN || S16;  // leaves are 16-bit codes (the 32-bit walk keeps them sign-extended)
   constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
   SphRcp rq;  // once per call: the sphere roots' divisor and its reciprocal
@@ -806,15 +801,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
   // near / far plane byte offsets inside DevNode4 by the ray's direction signs (32-bit offsets
   // from the uniform table base: the loads take the SGPR-base + VGPR-offset form)
-  uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
-  if constexpr (TS) {  // DevNode4t: a ray in the shutter's second half reads the split axis's planes at 128
-    if (r.time >= S.time_mid) {
-      const uint32_t ax = S.ts_axis;
-      nx = ax == 0u ? nx + 128u : nx;
-      ny = ax == 1u ? ny + 96u : ny;
-      nz = ax == 2u ? nz + 64u : nz;
-    }
-  }
+  const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
   const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes)
                                   : (HN ? reinterpret_cast<const char*>(S.hnodes) : reinterpret_cast<const char*>(S.nodes));
@@ -915,8 +902,7 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
             CW[2] = (int32_t)(int16_t)(cq.y & 0xFFFFu); CW[3] = (int32_t)cq.y >> 16;
           }
         } else {
-          // sizeof(DevNode4) or sizeof(DevNode4t); n_nodes < 2^25 (flatten)
-          const uint32_t nb = TS ? (uint32_t)ts.node * 160u : (uint32_t)ts.node << 7;
+          const uint32_t nb = (uint32_t)ts.node << 7;  // sizeof(DevNode4); n_nodes < 2^25 (flatten)
           constexpr uint32_t CWO = (K16 || S16) ? 112u : 96u;  // child codes (K16, S16) or child words
           const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx));
           const float4 qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
@@ -1378,13 +1364,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   constexpr int LST_ROWS = ((NCAP > 0 && BLK == 1024) || S16) ? 10 : 0;
   constexpr int LST_ROW0 = STACK + (S16 ? 1 : 0);
   __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1 + LST_ROWS) * BLK : 1)];
-  constexpr bool TS = ts_table(NCAP, HN);
-  constexpr uint32_t NODE_Q = HN ? 7u : (TS ? 10u : 8u);  // 16-B quads per node (DevNode4h / DevNode4t / DevNode4)
+  constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
   __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
-    const float4* g = HN   ? reinterpret_cast<const float4*>(a.scene.hnodes)
-                      : TS ? reinterpret_cast<const float4*>(a.scene.tnodes)
-                           : reinterpret_cast<const float4*>(a.scene.nodes);
+    const float4* g = HN ? reinterpret_cast<const float4*>(a.scene.hnodes) : reinterpret_cast<const float4*>(a.scene.nodes);
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * NODE_Q; k += BLK) nodes_lds[k] = g[k];
   }
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
@@ -1766,7 +1749,7 @@ int upload(Scene& s, int device) {
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
-  size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h), o_tnodes = put(blob, f.nodes4t);
+  size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h);
   blob.resize((blob.size() + 255) & ~(size_t)255);
   int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
   int prev = 0;
@@ -1786,9 +1769,6 @@ int upload(Scene& s, int device) {
     uint8_t* base = (uint8_t*)c.block;
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.hnodes = f.nodes4h.empty() ? nullptr : (const DevNode4h*)(base + o_hnodes);
-    c.scene.tnodes = f.nodes4t.empty() ? nullptr : (const DevNode4t*)(base + o_tnodes);
-    c.scene.time_mid = f.time_mid;
-    c.scene.ts_axis = f.ts_axis;
     c.scene.prims = (const DevPrim*)(base + o_prims);
     c.scene.always = (const uint32_t*)(base + o_always);
     c.scene.tshade = (const DevTriShade*)(base + o_tsh);
@@ -2433,17 +2413,6 @@ int rtw_diag_corrupt_bvh(rtw_scene* s, int device) {
   DeviceGuard g;
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemcpy(const_cast<DevNode4*>(c->scene.nodes), nd, sizeof nd, hipMemcpyHostToDevice), "hipMemcpy(nodes)");
-  if (c->scene.tnodes) {  // the LDS-node kernels' time-split table: the same cycle in both halves
-    DevNode4t tn[2];
-    for (int q = 0; q < 2; ++q) {
-      tn[q].n = nd[q];
-      const float* lo = c->scene.ts_axis == 0 ? nd[q].lo_x : (c->scene.ts_axis == 1 ? nd[q].lo_y : nd[q].lo_z);
-      const float* hi = c->scene.ts_axis == 0 ? nd[q].hi_x : (c->scene.ts_axis == 1 ? nd[q].hi_y : nd[q].hi_z);
-      memcpy(tn[q].alt_lo, lo, sizeof tn[q].alt_lo);
-      memcpy(tn[q].alt_hi, hi, sizeof tn[q].alt_hi);
-    }
-    HIPCHK(hipMemcpy(const_cast<DevNode4t*>(c->scene.tnodes), tn, sizeof tn, hipMemcpyHostToDevice), "hipMemcpy(tnodes)");
-  }
   if (c->scene.hnodes) {  // the half-precision table too: slot 0 = [-65504, +inf) on every axis, slots 1-3 empty
     DevNode4h hn[2];
     memset(hn, 0, sizeof hn);

@@ -61,9 +61,6 @@ struct Flat {
   bool codes16 = false;          // DevNode4::code holds valid 16-bit child codes (LDS-node kernels)
   uint32_t stack_need4 = 0;      // the same for the sorted-push walk of the LDS-node kernels (window of 4)
   std::vector<DevNode4h> nodes4h;  // nodes4 in half precision (when codes16; rtw_device.hpp)
-  std::vector<DevNode4t> nodes4t;  // nodes4 with one axis split at time_mid (when codes16; rtw_device.hpp)
-  uint32_t ts_axis = 1;
-  float time_mid = 0.5f;
   std::vector<DevPrim> prims;
   std::vector<DevShade> shade;  // per prim: material + common texture values (rtw_device.hpp)
   std::vector<uint32_t> always;
