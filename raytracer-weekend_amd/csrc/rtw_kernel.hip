@@ -1314,7 +1314,7 @@ __device__ __forceinline__ void fill_start_args(const RenderArgs& a, StartArgs& 
 
 // LST_BLK > 0: also store T = 1, depth and the path id in the lane's LDS state rows (path_kernel LST), here
 // where the values are made (carried to the caller, they were spilled)
-template <bool FROM_LDS, int LST_BLK = 0, int LST_ROW = 0, bool LRNG = false>
+template <bool FROM_LDS, int LST_BLK = 0, int LST_ROW = 0>
 __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, PathState& st, uint16_t* lst = nullptr) {
   if constexpr (FROM_LDS) asm volatile("" ::: "memory");  // read the LDS copy here: no loop-invariant register copies
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
@@ -1341,11 +1341,9 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
   st.depth = a.max_depth;
   st.pid = (uint32_t)pid;
   if constexpr (LST_BLK > 0) {
-    constexpr int NV = LRNG ? 7 : 5;  // LRNG: the RNG state too (rows 10-13)
-    const uint32_t v[7] = {0x3F800000u, 0x3F800000u, 0x3F800000u, a.max_depth, (uint32_t)pid, (uint32_t)rng,
-                           (uint32_t)(rng >> 32)};
+    const uint32_t v[5] = {0x3F800000u, 0x3F800000u, 0x3F800000u, a.max_depth, (uint32_t)pid};
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
+    for (int k = 0; k < 5; ++k) {
       lst[(LST_ROW + 2 * k) * LST_BLK] = (uint16_t)v[k];
       lst[(LST_ROW + 2 * k + 1) * LST_BLK] = (uint16_t)(v[k] >> 16);
     }
@@ -1363,10 +1361,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   __shared__ int32_t stk_all[(NCAP > 0 || S16) ? 1 : (STACK + 1) * BLK];
   // LST: 10 more 16-bit rows after the stack hold the path state (below)
   // (the S16 mesh walk too: its 16-bit stack column has STACK + 1 rows, the state rows follow them)
-  // LRNG (1024-lane LDS-node workgroups): 4 more rows hold the path's RNG state between shading passes
-  constexpr bool LRNG = NCAP > 0 && BLK == 1024;
-  static_assert(!LRNG || !(FEAT & F_MEDIUM), "LRNG: trace_run's segment key (media draws) is not kept");
-  constexpr int LST_ROWS = LRNG ? 14 : (S16 ? 10 : 0);
+  constexpr int LST_ROWS = ((NCAP > 0 && BLK == 1024) || S16) ? 10 : 0;
   constexpr int LST_ROW0 = STACK + (S16 ? 1 : 0);
   __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1 + LST_ROWS) * BLK : 1)];
   constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
@@ -1463,7 +1458,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, LRNG>(SA, id, st, stk16)) has = true;
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0>(SA, id, st, stk16)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1485,13 +1480,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
-    if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, LRNG ? 0ull : st.rng);
+    if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
     if (!(FEAT & F_LIST)) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
       const uint32_t leaf_thr = (act * a.leaf16 + 15u) >> 4;
       trace_run<COUNT, STACK, SPILL, FEAT, BLK, NCAP, HN, S16>(S, st.ray, ts, stk, spill, a.spill_lanes, cnt, quota,
-                                                      leaf_thr, LRNG ? 0ull : st.rng, a.err, ph + 4, nodes_lds, stk16);
+                                                      leaf_thr, st.rng, a.err, ph + 4, nodes_lds, stk16);
     } else {
       ts.node = -1;  // list mode: trace_begin tested every primitive
       ts.sp = 0;
@@ -1544,9 +1539,8 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const bool met = (FEAT & F_METAL) && mt == MT_METAL;
       const bool iso = (FEAT & F_ISO) && mt == MT_ISOTROPIC;
       V3 rs = mk(0.f, 0.f, 0.f);
-      uint64_t rng = LRNG ? ((uint64_t)lst_ld(6) << 32) | lst_ld(5) : st.rng;
       phase(2);
-      if (lam || met || iso) rs = rand_in_unit_sphere<SLDS>(rng);  // vec3.rs:101-108
+      if (lam || met || iso) rs = rand_in_unit_sphere<SLDS>(st.rng);  // vec3.rs:101-108
       phase(3);
       const V3 ud = unit(lam ? rs : st.ray.d);                  // Lambertian: unit(rs); else unit(d_in)
       V3 att = mk(1.f, 1.f, 1.f);                                 // Dielectric: attenuation (1,1,1)
@@ -1580,16 +1574,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           const float cos_t = fminf(dot(neg(ud), h.n), 1.0f);
           const float sin_t = sqrtf(1.0f - cos_t * cos_t);
           const bool cannot = (ratio * sin_t) > 1.0f;
-          if (cannot || reflectance(cos_t, r0) > gen_f32(rng)) dir = reflect(ud, h.n);
+          if (cannot || reflectance(cos_t, r0) > gen_f32(st.rng)) dir = reflect(ud, h.n);
           else dir = refract(ud, h.n, ratio);
         }
         const V3 T2 = mul(T, att);  // x * 1.0f == x: the Dielectric's T is unchanged
-        if constexpr (LRNG) {
-          lst_st(5, (uint32_t)rng);
-          lst_st(6, (uint32_t)(rng >> 32));
-        } else {
-          st.rng = rng;
-        }
         if constexpr (LST) {
           lst_st(0, __float_as_uint(T2.x));
           lst_st(1, __float_as_uint(T2.y));
