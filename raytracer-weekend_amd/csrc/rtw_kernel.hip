@@ -657,17 +657,11 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
 // A BVH leaf triangle when every leaf is a triangle of one wrapper chain (DevScene::bvh_tri): `lr` is
 // already the chain's object-space ray, no type dispatch; the 48 B of geometry in three loads, and the
 // tie key (DevPrim::key) only for a candidate at or below the best t (triangular.rs:97-138).
-// The normal n = ab x ac is recomputed from the loaded edges (the flattener's f32 products and differences in
-// the same order, no contraction: the same bits) instead of loaded: 36 B per test instead of 48, and the
-// vector-memory path's time follows the bytes its lanes load (profiles/r04/experiments u1).
 template <bool COUNT>
 __device__ __forceinline__ void test_tri_leaf(const DevScene& S, uint32_t pi, const Ray& lr, Best& b, uint32_t* cnt) {
   const float4* P = reinterpret_cast<const float4*>(S.prims + pi);
-  const float4 q0v = P[0], q1v = P[1];
-  const float acz = reinterpret_cast<const float*>(P + 2)[0];
-  const float abx = q0v.w, aby = q1v.x, abz = q1v.y, acx = q1v.z, acy = q1v.w;
-  const float q[12] = {q0v.x, q0v.y, q0v.z, abx, aby, abz, acx, acy, acz,
-                       aby * acz - abz * acy, abz * acx - abx * acz, abx * acy - aby * acx};
+  const float4 q0v = P[0], q1v = P[1], q2v = P[2];
+  const float q[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y, q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
   float u, v;
   const float t = cand_tri_uv(lr, q, u, v);
   if (COUNT) { cnt[1]++; cnt[2 + PT_TRI]++; simd_tick(cnt, 10, 11); }
