@@ -1634,6 +1634,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   }
 }
 
+#ifndef RTW_MESH_TU  // (rtw_kernel_mesh.hip compiles only the mesh path kernels: see pick_mesh)
 // Σ over samples in sample order (lib.rs:83-87), one thread per pixel of the pass.
 __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_slots) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1718,8 +1719,71 @@ __global__ void sweep_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long lon
   if (nbad) atomicAdd(n, nbad);
   if (nskip) atomicAdd(n + 1, nskip);
 }
+#endif  // RTW_MESH_TU
 
 }  // namespace dev
+
+// Variants of the path kernel: feature set x the waves per SIMD the register allocator must allow.
+// Sphere-only scenes (jumpy-balls) get the specialised kernel; everything else the generic one.
+// Trees whose push bound exceeds the LDS stack get the SPILL variant.  Default: 5 waves/SIMD.
+// Tuning knobs: RTW_OCC=4 (33-row stack) or RTW_OCC=6 (specialised kernel; spills registers);
+// RTW_STACK_LDS=4 selects a generic kernel with a 4-entry LDS stack, so that the HBM spill path
+// runs on every scene (tests/test_gpu_parity.py).
+typedef void (*path_fn)(RenderArgs);
+static int env_int(const char* k, int dflt) {
+  const char* e = getenv(k);
+  return e ? atoi(e) : dflt;
+}
+struct Variant {
+  path_fn fn;
+  uint32_t stack;        // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
+  uint32_t block = 256;  // workgroup size fn is compiled for
+  bool k16 = false;      // LDS-node kernel (sorted-push walk)
+};
+// LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
+// waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 224 node4s x 128 B + the pool
+// words = 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB): sphere worlds of up to ~850 spheres.
+constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
+// (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
+// from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
+template <bool C, uint32_t F>
+static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
+  using namespace dev;
+  if constexpr (F == F_MESHES) {
+    // 16-bit stack entries (the nodes' codes: half the LDS of the 32-bit stack, whose 31 KB per workgroup allow
+    // 5 per CU) and the paths' T / depth / id in LDS state rows, at 6 or 7 waves / SIMD (knob RTW_MESH_S16; 0 =
+    // the 32-bit stack at 5).  Measured (r04n, r04p): monument-4k +3.0% at 6 waves (80 VGPRs), +2.2% more with
+    // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows, so by default
+    // the half-node trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
+    const int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
+    if (codes16 && s16 >= 6 && need <= (uint32_t)STACK_DEEP5) {
+      const uint32_t st = (uint32_t)STACK_DEEP5;
+      if (s16 == 7)
+        return half ? Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st}
+                    : Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, false, true>, st};
+      return half ? Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, st}
+                  : Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, st};
+    }
+  }
+  if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built
+    if (half && need <= (uint32_t)STACK_LDS5)
+      return {path_kernel<C, STACK_LDS5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_LDS5};
+    if (half && need <= (uint32_t)STACK_DEEP5)
+      return {path_kernel<C, STACK_DEEP5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_DEEP5};
+  }
+  if (need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 5, F>, (uint32_t)STACK_LDS5};
+  if constexpr (F == F_MESHES || F == F_ALL) {
+    if (need <= (uint32_t)STACK_DEEP5) return {path_kernel<C, STACK_DEEP5, false, 5, F>, (uint32_t)STACK_DEEP5};
+    return {path_kernel<C, STACK_DEEP5, true, 5, F>, (uint32_t)STACK_DEEP5};
+  }
+  return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
+}
+// The mesh variants (F_MESHES) are compiled in their own translation unit, rtw_kernel_mesh.hip, with the
+// iterative-ILP machine scheduler instead of max-ILP (Makefile KFLAGS_MESH): cow +0.6%, monument +1.2%, where the
+// sphere and list-mode kernels lose 0.7-0.8% with it (profiles/r04/experiments k1)
+Variant pick_mesh(bool count, uint32_t need, bool half, bool codes16);
+
+#ifndef RTW_MESH_TU
 
 // ---------------------------------------------------------------- host side
 static int hip_fail(hipError_t e, const char* what) {
@@ -1860,61 +1924,6 @@ static uint64_t max_pass_paths() {
   return 1ull << l;
 }
 
-// Variants of the path kernel: feature set x the waves per SIMD the register allocator must allow.
-// Sphere-only scenes (jumpy-balls) get the specialised kernel; everything else the generic one.
-// Trees whose push bound exceeds the LDS stack get the SPILL variant.  Default: 5 waves/SIMD.
-// Tuning knobs: RTW_OCC=4 (33-row stack) or RTW_OCC=6 (specialised kernel; spills registers);
-// RTW_STACK_LDS=4 selects a generic kernel with a 4-entry LDS stack, so that the HBM spill path
-// runs on every scene (tests/test_gpu_parity.py).
-typedef void (*path_fn)(RenderArgs);
-static int env_int(const char* k, int dflt) {
-  const char* e = getenv(k);
-  return e ? atoi(e) : dflt;
-}
-struct Variant {
-  path_fn fn;
-  uint32_t stack;        // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
-  uint32_t block = 256;  // workgroup size fn is compiled for
-  bool k16 = false;      // LDS-node kernel (sorted-push walk)
-};
-// LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
-// waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 224 node4s x 128 B + the pool
-// words = 53,440 B per workgroup, 160,320 B per CU (<= 160 KiB): sphere worlds of up to ~850 spheres.
-constexpr int LDSN_STACK = 24, LDSN_CAP = 224, LDSN_BLK = 512;
-// (The spheres' 32-B test records in LDS too -- 18 stack rows, 512 x 32 B -- and the winner's hit record
-// from them measured equal within 0.2%: profiles/r02/experiments n6, h2.)
-template <bool C, uint32_t F>
-static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
-  using namespace dev;
-  if constexpr (F == F_MESHES) {
-    // 16-bit stack entries (the nodes' codes: half the LDS of the 32-bit stack, whose 31 KB per workgroup allow
-    // 5 per CU) and the paths' T / depth / id in LDS state rows, at 6 or 7 waves / SIMD (knob RTW_MESH_S16; 0 =
-    // the 32-bit stack at 5).  Measured (r04n, r04p): monument-4k +3.0% at 6 waves (80 VGPRs), +2.2% more with
-    // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows, so by default
-    // the half-node trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
-    const int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
-    if (codes16 && s16 >= 6 && need <= (uint32_t)STACK_DEEP5) {
-      const uint32_t st = (uint32_t)STACK_DEEP5;
-      if (s16 == 7)
-        return half ? Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st}
-                    : Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, false, true>, st};
-      return half ? Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, true, true>, st}
-                  : Variant{path_kernel<C, STACK_DEEP5, false, 6, F, BLOCK, 0, false, true>, st};
-    }
-  }
-  if constexpr (F == F_MESHES) {  // the half-precision node table (DevNode4h) where it was built
-    if (half && need <= (uint32_t)STACK_LDS5)
-      return {path_kernel<C, STACK_LDS5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_LDS5};
-    if (half && need <= (uint32_t)STACK_DEEP5)
-      return {path_kernel<C, STACK_DEEP5, false, 5, F, BLOCK, 0, true>, (uint32_t)STACK_DEEP5};
-  }
-  if (need <= (uint32_t)STACK_LDS5) return {path_kernel<C, STACK_LDS5, false, 5, F>, (uint32_t)STACK_LDS5};
-  if constexpr (F == F_MESHES || F == F_ALL) {
-    if (need <= (uint32_t)STACK_DEEP5) return {path_kernel<C, STACK_DEEP5, false, 5, F>, (uint32_t)STACK_DEEP5};
-    return {path_kernel<C, STACK_DEEP5, true, 5, F>, (uint32_t)STACK_DEEP5};
-  }
-  return {path_kernel<C, STACK_LDS5, true, 5, F>, (uint32_t)STACK_LDS5};
-}
 template <bool C>
 static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
                            bool codes16, bool has_half) {
@@ -1990,7 +1999,7 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
         // a partial LDS node cache (the top 128 / 376 / 760 node4s, the rest from global memory, sorted-push
         // walk) measured slower on cow / monument (profiles/r02/experiments, n7): the full-table kernels
         // are for trees that fit
-        return pick5<C, F_MESHES>(need, half, codes16);
+        return pick_mesh(C, need, half, codes16);
       }
       return pick5<C, F_ALL>(need);
   }
@@ -2282,8 +2291,10 @@ int enqueue_unpack(uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_t
   return RTW_OK;
 }
 
+#endif  // RTW_MESH_TU
 }  // namespace rtw
 
+#ifndef RTW_MESH_TU
 using namespace rtw;
 
 extern "C" {
@@ -2579,3 +2590,4 @@ int rtw_unpack_tiles_device(int device, uint32_t w, uint32_t h, const uint32_t* 
 }
 
 }  // extern "C"
+#endif  // RTW_MESH_TU
