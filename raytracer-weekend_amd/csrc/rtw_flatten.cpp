@@ -696,7 +696,7 @@ int flatten(Scene& s) {
     f.depth = bb.max_depth;
   }
   for (const Leaf& L : rest) f.prims.push_back(L.p);
-  for (const Leaf& L : huge) {  // the kernels rely on this: always[k] = prims.size() - always.size() + k
+  for (const Leaf& L : huge) {
     f.always.push_back((uint32_t)f.prims.size());
     f.prims.push_back(L.p);
   }

@@ -709,12 +709,8 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
     uint32_t cur = 0;
     Ray lr = r;
-    // the always-tested prims are the last n_always of the prim table, in order (rtw_flatten.cpp appends them
-    // after the BVH's): their indices need no load from S.always, so a prim's record loads do not wait on one
-    // (cornell-800 +4.7%: 18 prims per segment; cow +1.5%, monument +0.6%; experiments a1)
-    const uint32_t a0 = S.n_prims - S.n_always;
     for (uint32_t k = 0; k < S.n_always; ++k) {
-      const uint32_t pi = a0 + k;
+      const uint32_t pi = uload(S.always + k);
       const uint32_t inst = uload(&S.prims[pi].type_inst) >> 8;
       if (inst != cur) {
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
@@ -726,7 +722,6 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
     SphRcp rq;
     if constexpr (SPH_ONLY) rq = sph_rcp(r);
-    // (the loaded index here: the computed one made the sphere kernels 1.1% slower, experiments a1)
     for (uint32_t k = 0; k < S.n_always; ++k)
       test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
   }
