@@ -25,7 +25,8 @@ lib.rs:102, counted exactly by the kernel) / max-over-ranks step time.
 roofline is FP32 VALU: algorithmic flops per launch (SURVEY.md §8d / BASELINE.md: 21 per box
 tested, 23 per sphere test (+12 moving), 6 per rect, 51 per triangle, 70 per scattering segment,
 64 per path; DESIGN.md §5 itemises them) / the kernel's average HIP-event duration, vs the 157.3 TFLOP/s FP32 vector
-peak.  Reported beside it: the measured HBM fraction (rocprofv3 PMC bytes per launch / duration /
+peak, and as a second figure (`exact_f32_issue`) vs the 78.6 T lane-op/s a bit-exact kernel (no FMA contraction, no
+packed math: one lane-op per flop at best) can issue.  Reported beside them: the measured HBM fraction (rocprofv3 PMC bytes per launch / duration /
 8 TB/s), the SQ-counter VALU lane-capacity figure (VALU busy x lane utilisation) and the
 cache-level algorithmic bytes.  scripts/roofline.py recomputes all of them from profiles/.
 
@@ -65,7 +66,11 @@ CONFIGS = {
 SCENE_SEED = 42      # replaces thread_rng() in scenes.rs
 RENDER_SEED = 2024
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec)
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (spec): v_fma_f32 at 32 lanes/clk/SIMD, 2 flops each
+# The issue ceiling of an exact-f32 kernel: compiled -ffp-contract=off and without packed math, every
+# algorithmic flop is at least one non-FMA, non-packed VALU lane-op, and a SIMD-32 issues at most 32 lane-ops per
+# clock (MI355X_MICROARCH.md: a wave64 VALU instruction takes 2 cycles): 256 CUs x 4 SIMDs x 32 x 2.4 GHz
+EXACT_F32_ISSUE_T = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T lane-op/s
 # FP32 flop model (BASELINE.md roofline; DESIGN.md §5 derives each constant)
 FLOP_BOX = 21              # aabb.rs:23-48: per axis 1 div + 2 sub + 2 mul + min + max
 FLOP_PRIM = [23, 35, 6, 6, 6, 51]  # sphere (spherical.rs:26-44), moving (+12, :117-123), rect xy/xz/yz, triangle
@@ -164,6 +169,11 @@ def roofline(counts: dict, kernel_ms_per_launch: float, launches: int, world: in
            "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
            "flops_per_launch": round(flops), "kernel_ms_per_launch": round(kernel_ms_per_launch, 3),
            "flops_per_ray": round(flops_model(counts) / max(1, counts["rays"]), 1),
+           "exact_f32_issue": {"achieved": round(tflops, 3), "peak": round(EXACT_F32_ISSUE_T, 2), "unit": "T lane-op/s",
+                               "frac": round(tflops / EXACT_F32_ISSUE_T, 5),
+                               "note": "second figure: the algorithmic flops against the non-FMA, non-packed VALU lane "
+                                       "rate, the most a bit-exact (-ffp-contract=off, no packed math) kernel can issue "
+                                       "them at; frac above stays against the 157.3 TFLOP/s spec peak"},
            "hbm": None, "valu_lane": None, "vmem_units": None,
            "cache_level": {"alg_bytes_per_launch": round(alg_bytes),
                            "GBps": round(alg_bytes / (kernel_ms_per_launch * 1e-3) / 1e9, 1),

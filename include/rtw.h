@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 5
+#define RTW_ABI_VERSION 6
 
 enum {
   RTW_OK = 0,
@@ -248,6 +248,13 @@ int rtw_render_status(rtw_scene* s, int device);
 /* Test hook: overwrite the device copy's first two BVH nodes with a cycle, so that every render of it
  * trips the traversal guard (tests/test_gpu_parity.py).  The scene stays unusable on that device. */
 int rtw_diag_corrupt_bvh(rtw_scene* s, int device);
+/* Test hook (the multi-device path on a one-GPU node): before rtw_scene_commit, make the scene's devices n
+ * LOGICAL devices 0..n-1 that all live on physical device 0.  rtw_scene_commit(s, -1) then uploads n copies,
+ * each with its own stream, path queue, sample and packed buffers, so rtw_render_multi(s, n) runs its n > 1
+ * path (per-device renders, the grouped send/recv gather to logical device 0, the unpack) on one GPU.  Real
+ * RCCL refuses a clique whose ranks share a GPU: pair it with a loopback RCCL through RTW_RCCL_LIB
+ * (tests/loopback_rccl).  1 <= n <= 64, else RTW_EINVAL; RTW_ESTATE after the commit. */
+int rtw_diag_alias_devices(rtw_scene* s, int n);
 
 /* Raytracer::new(..).render().collect() (lib.rs:40-95) over n_gpus devices of this node, driven from
  * the calling host thread (the reference's Rayon pixel parallelism, lib.rs:57-76, becomes tiles

@@ -126,6 +126,7 @@ _SIGS = {
                                             C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
     "rtw_render_status": (C.c_int, [C.c_void_p, C.c_int]),
     "rtw_diag_corrupt_bvh": (C.c_int, [C.c_void_p, C.c_int]),
+    "rtw_diag_alias_devices": (C.c_int, [C.c_void_p, C.c_int]),
     "rtw_path_kernel_times": (C.c_int, [C.c_void_p, C.c_int, _F, C.c_uint32]),
     "rtw_render_multi": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rtw_camera), _F, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.c_uint32, C.c_uint64, _F, C.POINTER(rtw_stats)]),
@@ -157,7 +158,7 @@ EXPORTED_SYMBOLS = tuple(_SIGS)
 _lib = None
 
 
-ABI_VERSION = 5  # include/rtw.h RTW_ABI_VERSION
+ABI_VERSION = 6  # include/rtw.h RTW_ABI_VERSION
 
 
 def lib_sha() -> str:
@@ -428,6 +429,12 @@ class Scene:
     def diag_corrupt_bvh(self, device: int = -1) -> None:
         """Test hook: a cyclic BVH on the device copy (every render of it trips the guard)."""
         _check(lib().rtw_diag_corrupt_bvh(self._p, device))
+
+    def diag_alias_devices(self, n: int) -> "Scene":
+        """Test hook (before commit): n logical devices on physical device 0, so rtw_render_multi's n > 1
+        path runs on one GPU (with the loopback RCCL of tests/loopback_rccl via RTW_RCCL_LIB)."""
+        _check(lib().rtw_diag_alias_devices(self._p, int(n)))
+        return self
 
     def info(self, what: int) -> int:
         return int(lib().rtw_scene_info(self._p, what))

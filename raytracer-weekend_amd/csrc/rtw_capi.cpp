@@ -4,9 +4,12 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <new>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -23,6 +26,19 @@ int fail(int code, const char* fmt, ...) {
   vsnprintf(g_err, sizeof g_err, fmt, ap);
   va_end(ap);
   return code;
+}
+
+const char* tuning_env(const char* name) {
+  const char* v = getenv(name);
+  if (!v) return nullptr;
+  const char* gate = getenv("RTW_TUNING");
+  if (gate && !strcmp(gate, "1")) return v;
+  static std::mutex mu;  // one warning per knob name and process
+  static std::set<std::string> warned;
+  std::lock_guard<std::mutex> lock(mu);
+  if (warned.insert(name).second)
+    fprintf(stderr, "rtw: %s=%s ignored (tuning knobs are read only with RTW_TUNING=1)\n", name, v);
+  return nullptr;
 }
 
 static int check_open(rtw_scene* s) {

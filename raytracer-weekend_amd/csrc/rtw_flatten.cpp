@@ -326,10 +326,10 @@ struct BuildParams {
   int bins = 16;
   uint32_t pair = 2;  // ranges of at most this many prims become leaves without a SAH decision
   BuildParams() {
-    if (const char* e = getenv("RTW_BVH_PAIR")) pair = (uint32_t)std::min(4, std::max(1, atoi(e)));
-    if (const char* e = getenv("RTW_BVH_LEAF")) leaf_max = std::min(7, std::max(1, atoi(e)));
-    if (const char* e = getenv("RTW_BVH_TRAV")) trav = (float)atof(e);
-    if (const char* e = getenv("RTW_BVH_BINS")) bins = std::min(64, std::max(4, atoi(e)));
+    if (const char* e = tuning_env("RTW_BVH_PAIR")) pair = (uint32_t)std::min(4, std::max(1, atoi(e)));
+    if (const char* e = tuning_env("RTW_BVH_LEAF")) leaf_max = std::min(7, std::max(1, atoi(e)));
+    if (const char* e = tuning_env("RTW_BVH_TRAV")) trav = (float)atof(e);
+    if (const char* e = tuning_env("RTW_BVH_BINS")) bins = std::min(64, std::max(4, atoi(e)));
   }
 };
 constexpr int NBINS_MAX = 64;
@@ -634,7 +634,7 @@ int flatten(Scene& s) {
   // MI355X cornell-box (18 rects) renders 23% faster than through its 4-node BVH4 (14.6k ->
   // 17.9k Mrays/s).  Tuning knob RTW_LIST_MAX (0 = always build the BVH).
   uint32_t list_max = 32;
-  if (const char* e = getenv("RTW_LIST_MAX")) list_max = (uint32_t)std::min(64, std::max(0, atoi(e)));
+  if (const char* e = tuning_env("RTW_LIST_MAX")) list_max = (uint32_t)std::min(64, std::max(0, atoi(e)));
   if (B.leaves.size() <= list_max) {
     huge = B.leaves;
   } else if (B.leaves.size() > 16) {
@@ -668,7 +668,7 @@ int flatten(Scene& s) {
         if (inst == UINT32_MAX) inst = i;
         one_inst = one_inst && i == inst;
       }
-    const char* knob = getenv("RTW_TRI_LEAF");  // 0 = keep the mixed BVH and the generic leaf test
+    const char* knob = tuning_env("RTW_TRI_LEAF");  // 0 = keep the mixed BVH and the generic leaf test
     if ((!knob || atoi(knob)) && ntri > 16 && one_inst && rest.size() - ntri <= 4 &&
         huge.size() + (rest.size() - ntri) <= 8) {
       std::vector<Leaf> tris;
@@ -696,7 +696,7 @@ int flatten(Scene& s) {
     f.depth = bb.max_depth;
   }
   for (const Leaf& L : rest) f.prims.push_back(L.p);
-  for (const Leaf& L : huge) {
+  for (const Leaf& L : huge) {  // the kernels rely on this: always[k] = prims.size() - always.size() + k
     f.always.push_back((uint32_t)f.prims.size());
     f.prims.push_back(L.p);
   }

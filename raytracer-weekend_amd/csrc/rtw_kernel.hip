@@ -709,8 +709,12 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
     uint32_t cur = 0;
     Ray lr = r;
+    // the always-tested prims are the last n_always of the prim table, in order (rtw_flatten.cpp appends them
+    // after the BVH's): their indices need no load from S.always, so a prim's record loads do not wait on one
+    // (cornell-800 +4.7%: 18 prims per segment; cow +1.5%, monument +0.6%; experiments a1)
+    const uint32_t a0 = S.n_prims - S.n_always;
     for (uint32_t k = 0; k < S.n_always; ++k) {
-      const uint32_t pi = uload(S.always + k);
+      const uint32_t pi = a0 + k;
       const uint32_t inst = uload(&S.prims[pi].type_inst) >> 8;
       if (inst != cur) {
         lr = inst ? to_local<true>(S.insts + inst, r) : r;
@@ -722,6 +726,7 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     constexpr bool SPH_ONLY = (FEAT & (F_RECT | F_TRI | F_MEDIUM | F_INST)) == 0 && (FEAT & (F_SPHERE | F_MSPHERE));
     SphRcp rq;
     if constexpr (SPH_ONLY) rq = sph_rcp(r);
+    // (the loaded index here: the computed one made the sphere kernels 1.1% slower, experiments a1)
     for (uint32_t k = 0; k < S.n_always; ++k)
       test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
   }
@@ -1662,9 +1667,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RenderArgs a, uint32_t n_sl
   o[2] = z;
 }
 
-// The wavefront prototype (knob RTW_WAVEFRONT=1; measured slower, DESIGN.md §4 "Trace / shade split")
-#include "rtw_wavefront.inc"
-
 __global__ void unpack_tiles_kernel(uint32_t w, uint32_t h, uint32_t tiles_x, const uint32_t* tiles,
                                     uint32_t n_tiles, const float* packed, float* img) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1730,8 +1732,8 @@ __global__ void sweep_kernel(int fn, uint32_t lo, uint32_t hi, unsigned long lon
 // RTW_STACK_LDS=4 selects a generic kernel with a 4-entry LDS stack, so that the HBM spill path
 // runs on every scene (tests/test_gpu_parity.py).
 typedef void (*path_fn)(RenderArgs);
-static int env_int(const char* k, int dflt) {
-  const char* e = getenv(k);
+static int env_int(const char* k, int dflt) {  // a tuning knob (read only with RTW_TUNING=1)
+  const char* e = strcmp(k, "RTW_VERBOSE") ? tuning_env(k) : getenv(k);  // RTW_VERBOSE only prints
   return e ? atoi(e) : dflt;
 }
 struct Variant {
@@ -1755,8 +1757,12 @@ static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
     // the 32-bit stack at 5).  Measured (r04n, r04p): monument-4k +3.0% at 6 waves (80 VGPRs), +2.2% more with
     // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows, so by default
     // the half-node trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
-    const int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
-    if (codes16 && s16 >= 6 && need <= (uint32_t)STACK_DEEP5) {
+    int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
+    if (s16 != 0 && s16 != 6 && s16 != 7) {  //  no silent fallback for a value no variant has
+      fprintf(stderr, "rtw: RTW_MESH_S16=%d ignored (0, 6 or 7)\n", s16);
+      s16 = half ? 6 : 0;
+    }
+    if (codes16 && s16 != 0 && need <= (uint32_t)STACK_DEEP5) {
       const uint32_t st = (uint32_t)STACK_DEEP5;
       if (s16 == 7)
         return half ? Variant{path_kernel<C, STACK_DEEP5, false, 7, F, BLOCK, 0, true, true>, st}
@@ -1807,7 +1813,8 @@ int upload(Scene& s, int device) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(RTW_ENODEV, "no HIP device visible (the render core has no CPU fallback)");
-  if (device >= ndev) return fail(RTW_EINVAL, "device %d >= device count %d", device, ndev);
+  const int nlog = s.alias_n > 0 ? s.alias_n : ndev;  // logical devices (rtw_diag_alias_devices: all on 0)
+  if (device >= nlog) return fail(RTW_EINVAL, "device %d >= device count %d", device, nlog);
   const Flat& f = s.flat;
   std::vector<uint8_t> blob;
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
@@ -1815,13 +1822,15 @@ int upload(Scene& s, int device) {
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
   size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h);
   blob.resize((blob.size() + 255) & ~(size_t)255);
-  int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : ndev;
+  int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : nlog;
   int prev = 0;
   hipGetDevice(&prev);
   for (int d = d0; d < d1; ++d) {
-    HIPCHK(hipSetDevice(d), "hipSetDevice");
+    const int phys = s.alias_n > 0 ? 0 : d;
+    HIPCHK(hipSetDevice(phys), "hipSetDevice");
     DeviceCopy c;
     c.device = d;
+    c.phys = phys;
     c.bytes = blob.size();
     HIPCHK(hipMalloc(&c.block, c.bytes), "hipMalloc(scene)");
     HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
@@ -1865,7 +1874,7 @@ static void free_buf(DevBuf& b) {
 
 void release(Scene& s) {
   for (DeviceCopy& c : s.dev) {
-    if (hipSetDevice(c.device) != hipSuccess) continue;
+    if (hipSetDevice(c.phys) != hipSuccess) continue;
     if (c.block) hipFree(c.block);
     if (c.counters) hipFree(c.counters);
     if (c.err_host) hipHostFree(c.err_host);
@@ -1876,10 +1885,6 @@ void release(Scene& s) {
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
     for (void* e : c.gev)
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
-    for (void* e : c.wf_ev)
-      if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
-    if (c.wf_block) hipFree(c.wf_block);
-    if (c.wf_host) hipHostFree(c.wf_host);
     if (c.stream) hipStreamDestroy(static_cast<hipStream_t>(c.stream));
     for (auto& e : c.kev)
       for (void* x : e)
@@ -1919,7 +1924,7 @@ static int copy_events(DeviceCopy& c, hipEvent_t& e0, hipEvent_t& e1) {
 // with more paths (monument 4K x 1024 spp: 8.5 G, 2 passes) runs in several passes, each one persistent
 // launch + its in-order reduction.  Tuning knob RTW_PASS_LOG2 (24..33).
 static uint64_t max_pass_paths() {
-  const char* e = getenv("RTW_PASS_LOG2");
+  const char* e = tuning_env("RTW_PASS_LOG2");
   const int l = e ? std::min(32, std::max(24, atoi(e))) : 32;  // PathState::pid is 32-bit
   return 1ull << l;
 }
@@ -2020,7 +2025,7 @@ static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) 
   int per_cu = 0, cus = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)block, 0);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.phys) != hipSuccess || cus < 1) cus = 256;
   g = per_cu * cus;
   if (env_int("RTW_VERBOSE", 0))
     fprintf(stderr, "rtw: path kernel %p: block %u, %d resident blocks per CU x %d CUs\n", (void*)fn, block, per_cu, cus);
@@ -2045,80 +2050,6 @@ int check_guard(DeviceCopy& c) {
     *e = 0u;
     return fail(RTW_EINVAL, "a path kernel on device %d tripped its BVH traversal guard (corrupt tree?): the frame "
                 "it rendered is invalid", c.device);
-  }
-  return RTW_OK;
-}
-
-// The wavefront prototype's iterations for one pass (dev::WfArgs): trace + shade launches in chunks of 16
-// iterations; after each chunk the next iteration's ray-queue count and the path dispenser are copied to
-// pinned memory, and the chunk before it is checked (so the GPU always has a chunk queued): the pass is done
-// once no ray is queued and every path id has been handed out.
-static int run_wavefront(DeviceCopy& c, RenderArgs& a, hipStream_t stream) {
-  const uint32_t N = (uint32_t)std::min(1 << 26, std::max(1 << 12, env_int("RTW_WF_SLOTS", 1 << 21))) & ~1023u;
-  // a shard receives the appends of every 8th shading block (<= 2 x 1024 each: a scattered ray + a new path
-  // per thread at most, but no more than the block's 1024 items + its new paths, which are <= its finished ones)
-  const uint32_t cap = ((N / 1024u + 7u) / 8u) * 1024u;
-  constexpr int STACK = 16, BLK = 1024, NCAP = 144;
-  auto trace = dev::wf_trace_kernel<STACK, BLK, NCAP>;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace, BLK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus < 1) cus = 256;
-  const size_t E = (size_t)dev::WF_SHARDS * cap;  // entries per queue
-  const size_t need = 2 * E * (16 * 3 + 8) + E * 8 + 256;
-  if (need > c.wf_bytes) {
-    if (c.wf_block) HIPCHK(hipFree(c.wf_block), "hipFree(wavefront)");
-    c.wf_block = nullptr;
-    c.wf_bytes = 0;
-    HIPCHK(hipMalloc(&c.wf_block, need), "hipMalloc(wavefront)");
-    c.wf_bytes = need;
-  }
-  if (!c.wf_host) HIPCHK(hipHostMalloc((void**)&c.wf_host, 256, hipHostMallocDefault), "hipHostMalloc(wavefront)");
-  for (void*& e : c.wf_ev)
-    if (!e) {
-      hipEvent_t x;
-      HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming), "hipEventCreate");
-      e = x;
-    }
-  uint8_t* p = static_cast<uint8_t*>(c.wf_block);
-  dev::WfArgs wa;
-  for (int k = 0; k < 2; ++k) {
-    wa.q[k].o_t = reinterpret_cast<float4*>(p); p += E * 16;
-    wa.q[k].d_dep = reinterpret_cast<float4*>(p); p += E * 16;
-    wa.q[k].T_pid = reinterpret_cast<float4*>(p); p += E * 16;
-    wa.q[k].rng = reinterpret_cast<uint2*>(p); p += E * 8;
-  }
-  wa.hit = reinterpret_cast<uint2*>(p); p += E * 8;
-  wa.cnt = reinterpret_cast<uint32_t*>(p);
-  wa.n_slots = N;
-  wa.shard_cap = cap;
-  wa.par = 1;
-  wa.init = 1;
-  hipLaunchKernelGGL(dev::wf_init_kernel, dim3(1), dim3(64), 0, stream, wa);
-  const dim3 tgrid(per_cu * cus), sgrid(N / 1024);
-  // the first shading pass only starts N paths; its appends go to queue 0
-  hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(1024), 0, stream, a, wa);
-  HIPCHK(hipGetLastError(), "wavefront start");
-  wa.init = 0;
-  wa.par = 0;
-  const uint32_t chunk = (uint32_t)std::max(1, env_int("RTW_WF_CHUNK", 16));
-  for (uint32_t ch = 0;; ++ch) {
-    for (uint32_t k = 0; k < chunk; ++k) {
-      hipLaunchKernelGGL(trace, tgrid, dim3(BLK), 0, stream, a, wa);
-      hipLaunchKernelGGL(dev::wf_shade_kernel, sgrid, dim3(1024), 0, stream, a, wa);
-      wa.par ^= 1u;
-    }
-    HIPCHK(hipGetLastError(), "wavefront launches");
-    uint32_t* hb = c.wf_host + 32 * (ch & 1u);  // the next iteration's queue shard counts
-    HIPCHK(hipMemcpyAsync(hb, wa.cnt + wa.par * 8, 32, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(wavefront)");
-    HIPCHK(hipEventRecord(static_cast<hipEvent_t>(c.wf_ev[ch & 1u]), stream), "hipEventRecord");
-    if (ch >= 1) {
-      HIPCHK(hipEventSynchronize(static_cast<hipEvent_t>(c.wf_ev[(ch - 1) & 1u])), "wavefront progress");
-      const uint32_t* pb = c.wf_host + 32 * ((ch - 1) & 1u);
-      uint64_t rays = 0;
-      for (int s = 0; s < 8; ++s) rays += pb[s];
-      if (rays == 0) break;  // every dispenser is dry and every path done
-    }
-    if (ch > (1u << 22)) return fail(RTW_EINVAL, "wavefront: no progress");
   }
   return RTW_OK;
 }
@@ -2169,7 +2100,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   a.err = c.err_host;
   a.batch = (uint32_t)std::min(65536, std::max(64, env_int("RTW_BATCH", (int)dev::BATCH)));
   a.quota16 = 12;  // see trace_run (measured best of 4..16 on jumpy-balls); tuning knob RTW_QUOTA16 (1..16)
-  if (const char* q = getenv("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
+  if (const char* q = tuning_env("RTW_QUOTA16")) a.quota16 = (uint32_t)std::min(16, std::max(1, atoi(q)));
   // test postponed leaves once leaf16/16 of the wave's lanes hold one and cannot descend (trace_run);
   // knob RTW_LEAF16 (1..16)
   a.leaf16 = (uint32_t)std::min(16, std::max(1, env_int("RTW_LEAF16", 3)));  // LDS-node variants: 5, below
@@ -2232,8 +2163,6 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       c.spill_bytes = spill_bytes;
     }
     a.spill = c.spill;
-    // the wavefront prototype (knob RTW_WAVEFRONT=1): the 1024-lane LDS-node sphere worlds, plain renders only
-    const bool wavefront = env_int("RTW_WAVEFRONT", 0) == 1 && !count && var.k16 && var.block == 1024u;
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
@@ -2243,12 +2172,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
       HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
-      if (wavefront) {
-        if (int e = run_wavefront(c, a, stream)) return e;
-      } else {
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
-        HIPCHK(hipGetLastError(), "path_kernel launch");
-      }
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
+      HIPCHK(hipGetLastError(), "path_kernel launch");
       HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
       c.kev_head = (c.kev_head + 1) % 64u;
       c.kev_count = std::min(c.kev_count + 1u, 64u);
@@ -2321,7 +2246,7 @@ int rtw_render(rtw_scene* s, const rtw_camera* cam, const float bg[3], uint32_t 
   DeviceCopy* c = find_copy(s->s, -1);
   if (!c) return fail(RTW_ENODEV, "scene has no device copy");
   DeviceGuard g;
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   const size_t bytes = (size_t)w * h * 3 * sizeof(float);
   hipEvent_t e0, e1;
   if (int e = copy_events(*c, e0, e1)) return e;
@@ -2351,7 +2276,7 @@ static int render_device(rtw_scene* s, int device, const rtw_camera* cam, const 
   DeviceCopy* c = find_copy(s->s, device);
   if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
   DeviceGuard g;
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (stats)
     if (int e = copy_events(*c, e0, e1)) return e;
@@ -2396,7 +2321,7 @@ int rtw_render_status(rtw_scene* s, int device) {
   DeviceCopy* c = find_copy(s->s, device);
   if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
   DeviceGuard g;
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   HIPCHK(hipDeviceSynchronize(), "render (hipDeviceSynchronize)");
   return check_guard(*c);
 }
@@ -2422,7 +2347,7 @@ int rtw_diag_corrupt_bvh(rtw_scene* s, int device) {
     n.code[0] = 1u;
   }
   DeviceGuard g;
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   HIPCHK(hipMemcpy(const_cast<DevNode4*>(c->scene.nodes), nd, sizeof nd, hipMemcpyHostToDevice), "hipMemcpy(nodes)");
   if (c->scene.hnodes) {  // the half-precision table too: slot 0 = [-65504, +inf) on every axis, slots 1-3 empty
     DevNode4h hn[2];
@@ -2453,7 +2378,7 @@ int rtw_render_stream(rtw_scene* s, const rtw_camera* cam, const float bg[3], ui
   const uint32_t tiles_x = (w + 7u) / 8u, tiles_y = (h + 7u) / 8u;
   const uint32_t band_ty = std::max(1u, ((band_rows ? band_rows : 64u) + 7u) / 8u);  // tile rows per band
   DeviceGuard g;
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   const size_t band_tiles = (size_t)band_ty * tiles_x;
   if (int e = grow(c->packed, band_tiles * 64 * 3 * sizeof(float))) return e;
   float* d_packed = static_cast<float*>(c->packed.p);
@@ -2503,7 +2428,7 @@ int rtw_path_kernel_times(rtw_scene* s, int device, float* ms, uint32_t max_n) {
   if (!c) return fail(RTW_ENODEV, "scene was not committed to device %d", device);
   int prev = 0;
   hipGetDevice(&prev);
-  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipSetDevice(c->phys), "hipSetDevice");
   const uint32_t n = std::min(c->kev_count, max_n);
   int rc = (int)n;
   for (uint32_t q = 0; q < n; ++q) {  // the n most recent, oldest first

@@ -11,7 +11,10 @@
 //
 // RCCL is opened at the first render over more than one device (dlopen of librccl.so.1, or the file
 // named by RTW_RCCL_LIB), so the rest of the library -- rtw_render_multi(n_gpus = 1) included -- does
-// not depend on it.  The loader and the communicator cache are guarded by one mutex, and every use of a
+// not depend on it.  Under rtw_diag_alias_devices (a test hook) the n devices are logical devices on
+// physical device 0, so that this n > 1 path -- per-device streams, sample and packed buffers, the grouped
+// send/recv, the gather offsets, the unpack -- runs on a one-GPU box with the loopback RCCL stand-in of
+// tests/loopback_rccl (real RCCL refuses a clique whose ranks share a GPU).  The loader and the communicator cache are guarded by one mutex, and every use of a
 // clique's communicators (ncclGroupStart .. ncclGroupEnd) by that clique's own mutex, so host threads may
 // call rtw_render_multi concurrently on different scenes: RCCL communicators are not thread-safe, and two
 // interleaved grouped send/recv sequences on the same communicators could deadlock.
@@ -25,6 +28,7 @@
 #include <chrono>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -35,7 +39,7 @@ namespace rtw {
 namespace {
 
 struct Rccl {
-  bool tried = false;
+  std::string path;  // what was opened ("" = the default search)
   void* h = nullptr;
   ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
@@ -51,39 +55,49 @@ std::mutex& rccl_mutex() {
   return m;
 }
 
-// callers hold rccl_mutex()
-Rccl& rccl() {
-  static Rccl r;
-  if (r.tried) return r;
-  r.tried = true;
-  if (const char* lib = getenv("RTW_RCCL_LIB")) {  // knob: another RCCL build (or a missing one, in tests)
-    r.h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+// The RCCL library to use: librccl.so.1, or the file RTW_RCCL_LIB names (another RCCL build; a missing file in
+// tests; the loopback stand-in of tests/loopback_rccl for the one-GPU rehearsal).  Each library is opened once
+// and kept (communicators made by it stay valid); callers hold rccl_mutex().  NULL if it cannot be loaded.
+Rccl* rccl() {
+  static std::vector<std::unique_ptr<Rccl>> libs;
+  const char* want = getenv("RTW_RCCL_LIB");
+  const std::string path = want ? want : "";
+  for (auto& r : libs)
+    if (r->path == path) return r->h ? r.get() : nullptr;
+  auto r = std::make_unique<Rccl>();
+  r->path = path;
+  if (want) {
+    r->h = dlopen(want, RTLD_NOW | RTLD_LOCAL);
   } else {
     for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
-      r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
-      if (r.h) break;
+      r->h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (r->h) break;
     }
   }
-  if (!r.h) return r;
-  auto sym = [&](auto& fn, const char* n) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r.h, n)); };
-  sym(r.comm_init_all, "ncclCommInitAll");
-  sym(r.comm_destroy, "ncclCommDestroy");
-  sym(r.send, "ncclSend");
-  sym(r.recv, "ncclRecv");
-  sym(r.group_start, "ncclGroupStart");
-  sym(r.group_end, "ncclGroupEnd");
-  sym(r.error_string, "ncclGetErrorString");
-  if (!r.comm_init_all || !r.comm_destroy || !r.send || !r.recv || !r.group_start || !r.group_end || !r.error_string) {
-    dlclose(r.h);
-    r.h = nullptr;
+  if (r->h) {
+    auto sym = [&](auto& fn, const char* n) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r->h, n)); };
+    sym(r->comm_init_all, "ncclCommInitAll");
+    sym(r->comm_destroy, "ncclCommDestroy");
+    sym(r->send, "ncclSend");
+    sym(r->recv, "ncclRecv");
+    sym(r->group_start, "ncclGroupStart");
+    sym(r->group_end, "ncclGroupEnd");
+    sym(r->error_string, "ncclGetErrorString");
+    if (!r->comm_init_all || !r->comm_destroy || !r->send || !r->recv || !r->group_start || !r->group_end ||
+        !r->error_string) {
+      dlclose(r->h);
+      r->h = nullptr;
+    }
   }
-  return r;
+  libs.push_back(std::move(r));
+  return libs.back()->h ? libs.back().get() : nullptr;
 }
 
-// one communicator clique per device count, kept for the process (ncclCommInitAll is slow); each
+// one communicator clique per (library, HIP device list), kept for the process (ncclCommInitAll is slow); each
 // behind its own allocation, so a pointer handed out stays valid when the cache grows
 struct Clique {
-  int n = 0;
+  const Rccl* lib = nullptr;
+  std::vector<int> devs;
   std::vector<ncclComm_t> comms;
   std::mutex mu;  // held from ncclGroupStart through ncclGroupEnd of one gather
 };
@@ -97,27 +111,24 @@ std::vector<std::unique_ptr<Clique>>& cliques() {  // callers hold rccl_mutex()
     hipError_t e_ = (x);                                                            \
     if (e_ != hipSuccess) return fail(RTW_ENODEV, "%s: %s", what, hipGetErrorString(e_)); \
   } while (0)
-#define NCCLOK(x, what)                                                                       \
-  do {                                                                                        \
-    ncclResult_t r_ = (x);                                                                    \
-    if (r_ != ncclSuccess) return fail(RTW_ENODEV, "%s: %s", what, rccl().error_string(r_)); \
-  } while (0)
 
-int get_clique(int n, Clique** out) {
+// rank d of the clique is the communicator of the HIP device devs[d] (logical device d of the render)
+int get_clique(const std::vector<int>& devs, Clique** out) {
   std::lock_guard<std::mutex> lock(rccl_mutex());
+  const Rccl* r = rccl();
+  if (!r) return fail(RTW_ENODEV, "%s not loadable (a gather over %zu devices needs RCCL)",
+                      getenv("RTW_RCCL_LIB") ? getenv("RTW_RCCL_LIB") : "librccl.so.1", devs.size());
   for (auto& c : cliques())
-    if (c->n == n) {
+    if (c->lib == r && c->devs == devs) {
       *out = c.get();
       return RTW_OK;
     }
-  Rccl& r = rccl();
-  if (!r.h) return fail(RTW_ENODEV, "librccl.so.1 not loadable (a gather over %d devices needs RCCL)", n);
   auto c = std::make_unique<Clique>();
-  c->n = n;
-  c->comms.resize(n);
-  std::vector<int> devs(n);
-  for (int d = 0; d < n; ++d) devs[d] = d;
-  NCCLOK(r.comm_init_all(c->comms.data(), n, devs.data()), "ncclCommInitAll");
+  c->lib = r;
+  c->devs = devs;
+  c->comms.resize(devs.size());
+  const ncclResult_t e = r->comm_init_all(c->comms.data(), (int)devs.size(), devs.data());
+  if (e != ncclSuccess) return fail(RTW_ENODEV, "ncclCommInitAll: %s", r->error_string(e));
   *out = c.get();
   cliques().push_back(std::move(c));
   return RTW_OK;
@@ -148,8 +159,11 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   if (!s || !cam || !bg || !out) return fail(RTW_EINVAL, "NULL argument");
   if (!s->s.committed) return fail(RTW_ESTATE, "scene not committed");
   if (w < 2 || h < 2) return fail(RTW_EINVAL, "image must be at least 2x2 (lib.rs:84-85 divides by w-1, h-1)");
+  s->s.multi_ms.clear();  //  a failed call leaves no stale timings behind
+  s->s.multi_gather_ms = 0.0f;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RTW_ENODEV, "no HIP device visible");
+  if (s->s.alias_n > 0) ndev = s->s.alias_n;  // logical devices on physical device 0 (rtw_diag_alias_devices)
   const int n = n_gpus <= 0 ? ndev : n_gpus;
   if (n > ndev) return fail(RTW_EINVAL, "n_gpus %d > visible devices %d", n_gpus, ndev);
   std::vector<DeviceCopy*> cp(n);
@@ -168,7 +182,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   std::vector<hipEvent_t> e0(n), e1(n);
   for (int d = 0; d < n; ++d) {
     DeviceCopy& c = *cp[d];
-    HIPOK(hipSetDevice(d), "hipSetDevice");
+    HIPOK(hipSetDevice(c.phys), "hipSetDevice");
     if (!c.stream) {
       hipStream_t st;
       HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
@@ -188,7 +202,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
 
   if (n == 1) {  // one device: rtw_render's path (the whole frame straight into the image), no RCCL
     DeviceCopy& c = *cp[0];
-    HIPOK(hipSetDevice(0), "hipSetDevice");
+    HIPOK(hipSetDevice(c.phys), "hipSetDevice");
     hipStream_t st = static_cast<hipStream_t>(c.stream);
     if (int e = grow(c.image, frame_bytes)) return e;
     TileSet all;
@@ -208,9 +222,13 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   }
 
   Clique* clique = nullptr;
-  if (int e = get_clique(n, &clique)) return e;
+  {
+    std::vector<int> devs(n);
+    for (int d = 0; d < n; ++d) devs[d] = cp[d]->phys;
+    if (int e = get_clique(devs, &clique)) return e;
+  }
   const std::vector<ncclComm_t>* comms = &clique->comms;
-  const Rccl& r = rccl();  // loaded by get_clique; never changes afterwards
+  const Rccl& r = *clique->lib;  // loaded for good (rccl())
   const uint32_t per = (nt + (uint32_t)n - 1) / (uint32_t)n;  // padded tiles per device
   const size_t slot_floats = (size_t)per * 64 * 3;
   std::vector<uint32_t> all((size_t)n * per);
@@ -221,7 +239,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   // packed buffer on its own stream, all enqueued before any wait
   for (int d = 0; d < n; ++d) {
     DeviceCopy& c = *cp[d];
-    HIPOK(hipSetDevice(d), "hipSetDevice");
+    HIPOK(hipSetDevice(c.phys), "hipSetDevice");
     hipStream_t st = static_cast<hipStream_t>(c.stream);
     if (int e = grow(c.packed, slot_floats * sizeof(float))) return e;
     TileSet mt;
@@ -235,7 +253,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   }
   // 2. one RCCL gather to device 0 (each device's send waits for its render on the same stream)
   DeviceCopy& c0 = *cp[0];
-  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipSetDevice(c0.phys), "hipSetDevice");
   hipStream_t st0 = static_cast<hipStream_t>(c0.stream);
   if (int e = grow(c0.gathered, (size_t)n * slot_floats * sizeof(float))) return e;
   if (int e = grow(c0.gather_ids, all.size() * sizeof(uint32_t))) return e;
@@ -254,7 +272,8 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   HIPOK(hipEventRecord(static_cast<hipEvent_t>(c0.gev[0]), st0), "hipEventRecord");
   {
     std::lock_guard<std::mutex> lock(clique->mu);  // one grouped send/recv on these communicators at a time
-    NCCLOK(r.group_start(), "ncclGroupStart");
+    const ncclResult_t g0 = r.group_start();
+    if (g0 != ncclSuccess) return fail(RTW_ENODEV, "ncclGroupStart: %s", r.error_string(g0));
     for (int d = 0; d < n; ++d) {
       hipStream_t st = static_cast<hipStream_t>(cp[d]->stream);
       const ncclResult_t a = r.send(cp[d]->packed.p, slot_floats, ncclFloat32, 0, (*comms)[d], st);
@@ -270,12 +289,13 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
         return fail(RTW_ENODEV, "ncclRecv: %s", r.error_string(a));
       }
     }
-    NCCLOK(r.group_end(), "ncclGroupEnd");
+    const ncclResult_t g1 = r.group_end();
+    if (g1 != ncclSuccess) return fail(RTW_ENODEV, "ncclGroupEnd: %s", r.error_string(g1));
   }
-  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipSetDevice(c0.phys), "hipSetDevice");
   HIPOK(hipEventRecord(static_cast<hipEvent_t>(c0.gev[1]), st0), "hipEventRecord");
   // 3. device 0 scatters the gathered tiles into the frame and copies it out
-  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipSetDevice(c0.phys), "hipSetDevice");
   if (int e = enqueue_unpack(w, h, static_cast<uint32_t*>(c0.gather_ids.p), (uint32_t)all.size(), gathered,
                              static_cast<float*>(c0.image.p), st0))
     return e;
@@ -285,7 +305,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   memset(&tot, 0, sizeof tot);
   std::vector<float> dev_ms(n);
   for (int d = 0; d < n; ++d) {
-    HIPOK(hipSetDevice(d), "hipSetDevice");
+    HIPOK(hipSetDevice(cp[d]->phys), "hipSetDevice");
     rtw_stats st;
     memset(&st, 0, sizeof st);
     if (int e = collect_stats(*cp[d], cp[d]->stream, e0[d], e1[d], 0, &st)) return e;
@@ -294,7 +314,7 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
     dev_ms[d] = (float)st.kernel_ms;
   }
   float gms = 0.0f;
-  HIPOK(hipSetDevice(0), "hipSetDevice");
+  HIPOK(hipSetDevice(c0.phys), "hipSetDevice");
   HIPOK(hipEventElapsedTime(&gms, static_cast<hipEvent_t>(c0.gev[0]), static_cast<hipEvent_t>(c0.gev[1])),
         "hipEventElapsedTime(gather)");
   s->s.multi_ms = dev_ms;
@@ -302,6 +322,15 @@ int rtw_render_multi(rtw_scene* s, int n_gpus, const rtw_camera* cam, const floa
   tot.paths = (uint64_t)w * h * spp;
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = tot;
+  return RTW_OK;
+}
+
+// Test hook: n logical devices on physical device 0 (upload in rtw_kernel.hip; include/rtw.h)
+int rtw_diag_alias_devices(rtw_scene* s, int n) {
+  if (!s) return fail(RTW_EINVAL, "NULL argument");
+  if (s->s.committed) return fail(RTW_ESTATE, "scene already committed (alias the devices before the commit)");
+  if (n < 1 || n > 64) return fail(RTW_EINVAL, "n = %d logical devices (1..64)", n);
+  s->s.alias_n = n;
   return RTW_OK;
 }
 

@@ -86,7 +86,8 @@ struct DevBuf {  // a grow-only device allocation
 };
 
 struct DeviceCopy {
-  int device = -1;
+  int device = -1;  // the logical device the caller names (rtw_render_device, rtw_render_multi's device d)
+  int phys = -1;    // the HIP device it lives on: = device, except under rtw_diag_alias_devices (all on 0)
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
@@ -109,11 +110,6 @@ struct DeviceCopy {
   void* ev[2] = {nullptr, nullptr};        // hipEvent_t pair timing rtw_render / multi calls
   void* stream = nullptr;                  // hipStream_t of rtw_render_multi on this device
   void* gev[2] = {nullptr, nullptr};       // hipEvent_t pair around rtw_render_multi's gather (device 0)
-  // wavefront prototype (RTW_WAVEFRONT=1): slot state + queues, the host-visible progress words, their events
-  void* wf_block = nullptr;
-  size_t wf_bytes = 0;
-  uint32_t* wf_host = nullptr;             // pinned: per in-flight chunk, (rayq count, path ids taken lo, hi)
-  void* wf_ev[2] = {nullptr, nullptr};
 };
 
 struct Scene {
@@ -130,6 +126,8 @@ struct Scene {
   // gather ms (rtw_render_multi_times)
   std::vector<float> multi_ms;
   float multi_gather_ms = 0.0f;
+  // rtw_diag_alias_devices: > 0 = the scene's devices are this many logical devices on physical device 0
+  int alias_n = 0;
   Scene() { nodes.push_back(Node{NK_LIST, {}}); }
 };
 
@@ -164,6 +162,11 @@ int enqueue_unpack(uint32_t w, uint32_t h, const uint32_t* d_tiles, uint32_t n_t
 
 // thread-local error reporting (rtw_capi.cpp)
 int fail(int code, const char* fmt, ...);
+// A tuning knob's value (RTW_OCC, RTW_BATCH, RTW_LIST_MAX, ...: DESIGN.md §4), or NULL.  The knobs select
+// kernel variants and scheduling parameters for A/B measurements; they are read only when RTW_TUNING=1, so a
+// process that inherits a stray variable still runs the default (measured-best) kernels.  A knob set without
+// the gate is ignored with one warning on stderr (rtw_capi.cpp).
+const char* tuning_env(const char* name);
 
 }  // namespace rtw
 

@@ -2,6 +2,7 @@
 #   usage: TAG=x_ CONFIGS="jumpy-1080p monument-4k" VARIANTS="RTW_OCC=5 RTW_OCC=6|RTW_QUOTA16=10" bash scripts/gpu_ab.sh
 #   (one variant per word; "|" joins several variables of one variant)
 set -o pipefail
+export RTW_TUNING=1  # the library reads tuning knobs only with the gate open
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 TAG=${TAG:-ab_}

@@ -55,3 +55,11 @@ def gpu(rtw):
     # -m gpu runs on the MI355X box: a missing device is a failure, never a silent skip
     assert rtw.device_count() >= 1, "no HIP device visible for a gpu-marked test"
     return rtw
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    """monkeypatch with the tuning gate open: the product library reads its RTW_* tuning knobs (kernel
+    variants, scheduling parameters, SAH build knobs) only when RTW_TUNING=1."""
+    monkeypatch.setenv("RTW_TUNING", "1")
+    return monkeypatch

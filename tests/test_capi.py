@@ -256,12 +256,12 @@ def test_half_nodes_beyond_f16_range(rtw, offset, built):
 
 
 @pytest.mark.parametrize("knob", ["RTW_BVH_PAIR=1", "RTW_BVH_PAIR=3", "RTW_BVH_BINS=64", "RTW_BVH_LEAF=2"])
-def test_bvh_build_knobs_cover_every_prim(rtw, monkeypatch, knob):
+def test_bvh_build_knobs_cover_every_prim(rtw, knobs, knob):
     """The SAH build knobs (RTW_BVH_PAIR / BINS / LEAF) only reshape the tree: the flattener's own
     self-check (every node4 reached once, every BVH prim in exactly one leaf) passes, the leaves' prim ranges
     cover the BVH part once, and the 16-bit codes still hold (leaves of <= 4 prims)."""
     k, v = knob.split("=")
-    monkeypatch.setenv(k, v)
+    knobs.setenv(k, v)
     for name in ("jumpy-balls", "wavefront-cow-obj"):
         s = rtw.Scene()
         s.preset(name, 16 / 9, seed=42)
@@ -276,3 +276,33 @@ def test_bvh_build_knobs_cover_every_prim(rtw, monkeypatch, knob):
             cover[f:f + c] += 1
         assert np.all(cover == 1), name
         assert s.info(11) >= 4
+
+
+def test_tuning_knobs_need_the_gate(rtw, monkeypatch, capfd):
+    """a stray tuning variable must not change the product's kernels.  RTW_LIST_MAX=0 (BVH
+    instead of list mode, read by the flattener at commit) takes effect only with RTW_TUNING=1; without the
+    gate it is ignored with a warning on stderr, and cornell-box stays a BVH-less list-mode world."""
+    monkeypatch.delenv("RTW_TUNING", raising=False)
+    monkeypatch.setenv("RTW_LIST_MAX", "0")
+    s = rtw.Scene()
+    s.preset("cornell-box", 1.0, seed=3)
+    _commit_anywhere(rtw, s)
+    assert s.info(3) == 0 and s.info(5) > 0  # list mode: no BVH nodes, every prim always tested
+    assert "RTW_LIST_MAX=0 ignored" in capfd.readouterr().err
+    monkeypatch.setenv("RTW_TUNING", "1")
+    s = rtw.Scene()
+    s.preset("cornell-box", 1.0, seed=3)
+    _commit_anywhere(rtw, s)
+    assert s.info(3) > 0  # the knob applies: a BVH over the rects
+
+
+def test_alias_devices_arguments(rtw):
+    """rtw_diag_alias_devices (the one-GPU rehearsal of rtw_render_multi, tests/test_gpu_multi.py): 1..64
+    logical devices, before the commit only."""
+    s = rtw.Scene()
+    for bad in (0, -1, 65):
+        with pytest.raises(rtw.RtwError) as e:
+            s.diag_alias_devices(bad)
+        assert e.value.code == rtw.RTW_EINVAL
+    s.diag_alias_devices(8)
+    s.diag_alias_devices(2)  # may be changed until the commit

@@ -72,14 +72,14 @@ def _sphere_cloud(rtw, n=200, seed=4):
 
 
 @pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0"])
-def test_corrupt_bvh_fails_every_path(gpu, monkeypatch, knob):
+def test_corrupt_bvh_fails_every_path(gpu, knobs, knob):
     """A cyclic node table (rtw_diag_corrupt_bvh) trips the traversal guard.  Renders enqueued
     without stats (bench.py's timed frames, the torchrun N>1 path) return RTW_OK, and the fault
     surfaces at rtw_render_status, at the next render call and at rtw_path_kernel_times; a render with
     stats fails itself.  Both walks: the LDS-node kernel (16-bit codes) and the global-node one."""
     torch = pytest.importorskip("torch")
     if knob:
-        monkeypatch.setenv(*knob.split("="))
+        knobs.setenv(*knob.split("="))
     rtw = gpu
     s, cam, bg = _sphere_cloud(rtw)
     s.commit(device=0)
@@ -109,7 +109,7 @@ def test_corrupt_bvh_fails_every_path(gpu, monkeypatch, knob):
 
 
 @pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0"])
-def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, monkeypatch, knob):
+def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, knobs, knob):
     """after a guard trip the kernel closes the path queue and empties the wave's id pool, so a
     large corrupt frame costs about one trip per wave, not one per 64 paths.  A 256x256x16 frame (16 K
     64-path groups, ~1 K waves with work) must take at most 8x the time of an 8x8x1 frame (one wave, one
@@ -117,7 +117,7 @@ def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, monkeypatch, knob
     import time
     torch = pytest.importorskip("torch")
     if knob:
-        monkeypatch.setenv(*knob.split("="))
+        knobs.setenv(*knob.split("="))
     rtw = gpu
     s, cam, bg = _sphere_cloud(rtw)
     s.commit(device=0)

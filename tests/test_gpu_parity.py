@@ -103,10 +103,10 @@ def test_error_paths(gpu):
 
 
 @pytest.mark.parametrize("name,aspect,w,h,spp", [SCENES[0], SCENES[2], SCENES[3]])
-def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
+def test_stack_spill_bit_exact(gpu, orc, knobs, name, aspect, w, h, spp):
     """A 4-entry LDS stack pushes every deeper entry through the HBM spill area
     (RenderArgs::spill); the image must not change."""
-    monkeypatch.setenv("RTW_STACK_LDS", "4")
+    knobs.setenv("RTW_STACK_LDS", "4")
     g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
     assert st["rays"] == rays
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
@@ -118,7 +118,7 @@ def test_stack_spill_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
                                   "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7",
                                   "RTW_LDSN_BLK=512", "RTW_MESH_S16=0", "RTW_MESH_S16=6",
                                   "RTW_MESH_S16=7", "RTW_BVH_PAIR=1", "RTW_BVH_BINS=64"])
-def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
+def test_scheduling_knobs_bit_exact(gpu, orc, knobs, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
     operations are keyed by its (pixel, sample) id, so the image and the ray count must not move.
@@ -127,7 +127,7 @@ def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
     RTW_BVH_BINS): closest hit with ties to the later object is a commutative reduction over the leaves,
     whatever culls them."""
     k, v = knob.split("=")
-    monkeypatch.setenv(k, v)
+    knobs.setenv(k, v)
     # the half-node knobs matter for BVH worlds: jumpy-balls (LDS nodes) and the cow (global nodes)
     mesh = "HALF" in k or "TRI" in k or "MESH" in k or "BVH" in k
     for name, aspect, w, h, spp in ((SCENES[0], SCENES[2], SCENES[3]) if mesh else (SCENES[0], SCENES[1])):
@@ -136,21 +136,7 @@ def test_scheduling_knobs_bit_exact(gpu, orc, monkeypatch, knob):
         assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
 
 
-@pytest.mark.parametrize("slots", ["", "4096", "65536"])
-def test_wavefront_prototype_bit_exact(gpu, orc, monkeypatch, slots):
-    """RTW_WAVEFRONT=1: the trace / shade split across kernels with the slot state and
-    the ray / free-slot queues in global memory renders the same image and ray count as the oracle; small
-    slot counts (RTW_WF_SLOTS) force many iterations, slot reuse and the end-of-frame drain."""
-    monkeypatch.setenv("RTW_WAVEFRONT", "1")
-    if slots:
-        monkeypatch.setenv("RTW_WF_SLOTS", slots)
-    name, aspect, w, h, spp = SCENES[0]
-    g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
-    assert st["rays"] == rays
-    assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), name
-
-
-def test_pass_with_path_ids_above_2_31(gpu, monkeypatch):
+def test_pass_with_path_ids_above_2_31(gpu, knobs):
     """One pass of more than 2^31 paths (monument-4k's passes hold 2^32): path ids past 2^31 must
     dispense and index correctly.  The same frame split into 2^30-path passes is the reference."""
     rtw = gpu
@@ -160,7 +146,7 @@ def test_pass_with_path_ids_above_2_31(gpu, monkeypatch):
     w = h = 256
     spp = 32800  # 256 * 256 * 32800 = 2.15e9 paths > 2^31
     one, st1 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=7).render()
-    monkeypatch.setenv("RTW_PASS_LOG2", "30")
+    knobs.setenv("RTW_PASS_LOG2", "30")
     split, st2 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=7).render()
     assert st1["rays"] == st2["rays"] > w * h * spp
     assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
@@ -180,10 +166,10 @@ def test_path_kernel_times(gpu):
 
 
 @pytest.mark.parametrize("name,aspect,w,h,spp", [SCENES[1], SCENES[2], SCENES[3], SCENES[5]])
-def test_generic_kernel_bit_exact(gpu, orc, monkeypatch, name, aspect, w, h, spp):
+def test_generic_kernel_bit_exact(gpu, orc, knobs, name, aspect, w, h, spp):
     """Every scene normally runs the smallest specialised kernel variant covering its features
     (F_SPHERES / F_BOXES / F_MESHES, rtw_device.hpp); the all-features kernel must agree too."""
-    monkeypatch.setenv("RTW_GENERIC", "1")
+    knobs.setenv("RTW_GENERIC", "1")
     g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
     assert st["rays"] == rays
     assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
@@ -372,7 +358,7 @@ def _sphere_world(rtw, seed, n=120):
 @pytest.mark.parametrize("knob", ["", "RTW_LDS_NODES=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7", "RTW_HALF_NODES=1",
                                   "RTW_LDSN_BLK=512", "RTW_BVH_PAIR=1"])
 @pytest.mark.parametrize("seed,n", [(1, 120), (2, 120), (3, 700)])
-def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
+def test_random_sphere_world_bit_exact(gpu, orc, knobs, knob, seed, n):
     """Sphere worlds run the LDS-node kernel (node table in LDS, sorted-push walk over 16-bit codes)
     when their tree fits -- the 8-wave variant for trees of <= 144 node4s (the 120-sphere worlds: 1024-lane
     workgroups with the paths' T / depth / id in LDS, or the 512-lane form by knob), the
@@ -381,7 +367,7 @@ def test_random_sphere_world_bit_exact(gpu, orc, monkeypatch, knob, seed, n):
     specialise for; likewise the 6 / 7-wave and half-precision-node variants by knob."""
     if knob:
         k, v = knob.split("=")
-        monkeypatch.setenv(k, v)
+        knobs.setenv(k, v)
     rtw = gpu
     s, cam, bg = _sphere_world(rtw, seed, n)
     text = s.dump()
@@ -411,10 +397,10 @@ def test_fast_reciprocal_equals_ieee_for_every_float(gpu):
 
 @pytest.mark.parametrize("case", ["far_plane", "far_origin", "near"])
 def test_rect_reciprocal_guard_paths_bit_exact(gpu, orc, case):
-    """The list-mode rect test divides by Markstein's correction from per-chain reciprocals of the ray
-    direction (cand_rect_rcp), guarded per chain: a rect plane |k| >= 2^62 (DevScene::rect_k_small = 0)
-    or a ray origin |o_k| >= 2^62 sends every lane to the IEEE division.  All three cases, with
-    wrapper chains (a rotated, translated cuboid), must match the oracle bit for bit."""
+    """Rect tests at the edges of f32's range (rectangular.rs:27-57, :78-108, :129-159): a sky plane at
+    |k| = 1e19, camera rays whose origin is 1e19 away, and near planes, each with a wrapper chain (a rotated,
+    translated cuboid) in list mode, must match the oracle bit for bit: the rect test's IEEE divisions
+    (k - o) / d and its bounds must round exactly as the reference's at huge and tiny quotients."""
     rtw = gpu
     s = rtw.Scene()
     red = s.lambertian_solid((0.65, 0.05, 0.05))
