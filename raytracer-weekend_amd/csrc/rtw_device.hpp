@@ -185,7 +185,7 @@ struct DevScene {
   uint32_t msphere_unit;  // every moving sphere's shutter is [+0, 1]: center_at needs no q2 / division
   uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
   float uni_off[3];
-  uint32_t reserved0;     // (was rect_k_small, round 3's dropped reciprocal rect test; keeps the kernarg layout)
+  uint32_t rect_k_small;  // every rect plane has |k| < 2^62 (the list-mode rect loop's reciprocal division guard)
   uint32_t bvh_tri;       // every BVH leaf primitive is a triangle of instance tri_inst (the leaf fast path)
   uint32_t tri_inst;
 };

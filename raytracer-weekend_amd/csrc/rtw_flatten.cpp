@@ -701,6 +701,12 @@ int flatten(Scene& s) {
     f.prims.push_back(L.p);
   }
   if (f.depth > MAX_DEPTH) return fail(RTW_EINVAL, "BVH deeper than the traversal stack (%u)", f.depth);
+  // the list-mode rect loop (rtw_kernel.hip trace_rect_list) accepts t <= best: a later prim of the list must
+  // have the larger DFS key, which holds because list mode keeps the leaves in walk (= key) order
+  if (f.nodes.empty())
+    for (size_t k = 1; k < f.always.size(); ++k)
+      if (!(f.prims[f.always[k]].key > f.prims[f.always[k - 1]].key))
+        return fail(RTW_EINVAL, "internal: list-mode prims out of key order");
   // triangle shading data re-indexed by prim (tshade[k] belongs to prims[k]): the winner's
   // normals / uvs load straight from the hit's prim index, beside its geometry
   if (!f.tshade.empty()) {
@@ -712,6 +718,13 @@ int flatten(Scene& s) {
         f.prims[k].aux = (uint32_t)k;
       }
     f.tshade.swap(by_prim);
+  }
+  // the list-mode rect loop divides by Markstein's correction where |k - o| < 2^64 is guaranteed: |o| < 2^62
+  // per lane (checked by the kernel) and |k| < 2^62 for every rect plane (here)
+  f.rect_k_small = 1;
+  for (const DevPrim& p : f.prims) {
+    const uint32_t t = p.type_inst & 0xffu;
+    if ((t == PT_RECT_XY || t == PT_RECT_XZ || t == PT_RECT_YZ) && !(fabsf(p.q1[0]) < 0x1p62f)) f.rect_k_small = 0;
   }
   // spheres carry their DFS key in q1[3] too (the sphere-only kernels' 32-B test, rtw_device.hpp)
   for (DevPrim& p : f.prims) {

@@ -700,11 +700,98 @@ struct TraceState {
   bool on;       // a traversal is in progress
 };
 
+// One rect of the list-mode rect loop (rectangular.rs:27-57, :78-108, :129-159): t = (k - o_k) / d_k, the hit
+// point's two other coordinates, the bounds, and the accept (hittable/mod.rs:61-65) against the best so far.
+// `fast` (wave-uniform): the division is Markstein's correction from y_k = RN(1 / d_k), exact for the whole wave
+// (see trace_rect_list); else the IEEE division.  The list is in DFS-key order, so a later rect wins a tie: the
+// accept is t <= best.  bt starts at FLT_MAX, which also rejects t = inf and NaN.
+template <int AXIS>
+__device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, bool fast, float4 q0, float k, uint32_t pi,
+                                               float& bt, int32_t& bp) {
+  const float o_k = AXIS == 0 ? lr.o.z : (AXIS == 1 ? lr.o.y : lr.o.x);
+  const float d_k = AXIS == 0 ? lr.d.z : (AXIS == 1 ? lr.d.y : lr.d.x);
+  const float y_k = AXIS == 0 ? y.z : (AXIS == 1 ? y.y : y.x);
+  const float o_a = AXIS == 2 ? lr.o.y : lr.o.x, d_a = AXIS == 2 ? lr.d.y : lr.d.x;
+  const float o_b = AXIS == 0 ? lr.o.y : lr.o.z, d_b = AXIS == 0 ? lr.d.y : lr.d.z;
+  const float num = k - o_k;
+  float t;
+  if (fast) t = div_by_recip(num, d_k, y_k);
+  else t = num / d_k;
+  const float x = o_a + t * d_a;
+  const float yy = o_b + t * d_b;
+  const bool out = (x < q0.x) | (x > q0.y) | (yy < q0.z) | (yy > q0.w);
+  const bool acc = (t >= TMIN) & (t <= bt) & !out;
+  bt = acc ? t : bt;
+  bp = acc ? (int32_t)pi : bp;
+}
+
+// The list-mode loop of rect worlds (cornell-box: the F_BOXES | F_LIST kernel).  Per wrapper chain (a Cuboid's
+// six sides are adjacent) the object-space ray and the reciprocals y = RN(1 / d) of its three direction
+// components (rcp_rn_fast: exact in [2^-126, 2^126]); each rect's division (k - o_k) / d_k is then Markstein's
+// correction from y_k (3 VALU) instead of the IEEE division (11).  It is the IEEE quotient whenever
+// |d_k| in [2^-60, 2^60] and |k - o_k| < 2^64 (|k| < 2^62 for every rect: DevScene::rect_k_small; |o_k| < 2^62
+// per lane): then no step over- or underflows unless |quotient| < 2^-42, where both are < TMIN and rejected
+// alike (Markstein 1990; div_by_recip).  A chain where any lane of the wave is outside that range takes the IEEE
+// division for the whole wave (a scalar branch, no per-rect exec masking).
+// The rect test's bounds and the accept are one set of compares and two selects (the key is not needed: the
+// list is in DFS-key order).  VERDICT r4 item 3.
+template <bool COUNT>
+__device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r, Best& best, uint32_t* cnt) {
+  float bt = 0x1.fffffep127f;  // FLT_MAX
+  int32_t bp = -1;
+  uint32_t cur = 0xFFFFFFFFu;
+  Ray lr = r;
+  V3 y = mk(0.f, 0.f, 0.f);
+  bool fast = false;
+  const uint32_t a0 = S.n_prims - S.n_always;  // the always-tested prims are the table's last (rtw_flatten.cpp)
+  // the whole 64-B record in one scalar load (s_load_dwordx16): one round trip per rect
+  typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+  auto ld_rec = [&](uint32_t pi) -> u16v { return *(const __attribute__((address_space(4))) u16v*)(S.prims + pi); };
+#ifndef RTW_RECT_PIPE
+#define RTW_RECT_PIPE 0
+#endif
+  u16v nxt;
+  if (RTW_RECT_PIPE && S.n_always) nxt = ld_rec(a0);
+  for (uint32_t k = 0; k < S.n_always; ++k) {
+    const uint32_t pi = a0 + k;
+    u16v rec;
+    if (RTW_RECT_PIPE) {  // (experiment) the next rect's record loads while this one is tested
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this rect's record (and nothing else) has arrived
+      rec = nxt;
+      nxt = ld_rec(min(pi + 1u, S.n_prims - 1u));
+    } else {
+      rec = ld_rec(pi);
+    }
+    const float4 q0 = make_float4(__uint_as_float(rec[0]), __uint_as_float(rec[1]), __uint_as_float(rec[2]),
+                                  __uint_as_float(rec[3]));
+    const float4 q1 = make_float4(__uint_as_float(rec[4]), 0.f, 0.f, 0.f);
+    const uint32_t inst = rec[12] >> 8, type = rec[12] & 0xffu;
+    if (inst != cur) {  // wave-uniform
+      cur = inst;
+      lr = inst ? to_local<true>(S.insts + inst, r) : r;
+      y = mk(rcp_rn_fast(lr.d.x), rcp_rn_fast(lr.d.y), rcp_rn_fast(lr.d.z));
+      const bool ok = recip_div_ok(lr.d.x) && recip_div_ok(lr.d.y) && recip_div_ok(lr.d.z) &&
+                      fabsf(lr.o.x) < 0x1p62f && fabsf(lr.o.y) < 0x1p62f && fabsf(lr.o.z) < 0x1p62f;
+      fast = S.rect_k_small && __ballot(!ok) == 0;
+    }
+    if (type == PT_RECT_XY) rect_list_test<0>(lr, y, fast, q0, q1.x, pi, bt, bp);
+    else if (type == PT_RECT_XZ) rect_list_test<1>(lr, y, fast, q0, q1.x, pi, bt, bp);
+    else rect_list_test<2>(lr, y, fast, q0, q1.x, pi, bt, bp);
+    if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }
+  }
+  best.t = bt;
+  best.prim = bp;
+}
+
 template <bool COUNT, uint32_t FEAT>
 __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
                                             uint64_t seg) {
   ts.b = Best{INFINITY, 0u, -1, 0.0f, 0.0f};
-  if (FEAT & F_INST) {
+  // list-mode worlds of rects only (the F_BOXES | F_LIST kernel)
+  constexpr bool RECT_LIST = (FEAT & F_LIST) && (FEAT & F_RECT) && !(FEAT & (F_SPHERE | F_MSPHERE | F_TRI | F_MEDIUM));
+  if constexpr (RECT_LIST) {
+    trace_rect_list<COUNT>(S, r, ts.b, cnt);
+  } else if (FEAT & F_INST) {
     // the always list is wave-uniform and in DFS order, so a wrapper chain's prims are adjacent
     // (a Cuboid's 6 sides): transform the ray once per chain instead of once per prim
     uint32_t cur = 0;
@@ -1319,7 +1406,7 @@ __device__ __forceinline__ void fill_start_args(const RenderArgs& a, StartArgs& 
 
 // LST_BLK > 0: also store T = 1, depth and the path id in the lane's LDS state rows (path_kernel LST), here
 // where the values are made (carried to the caller, they were spilled)
-template <bool FROM_LDS, int LST_BLK = 0, int LST_ROW = 0>
+template <bool FROM_LDS, int LST_BLK = 0, int LST_ROW = 0, bool AB = FROM_LDS>
 __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, PathState& st, uint16_t* lst = nullptr) {
   if constexpr (FROM_LDS) asm volatile("" ::: "memory");  // read the LDS copy here: no loop-invariant register copies
   const uint32_t hi = (uint32_t)(pid >> 6), l = (uint32_t)pid & 63u;
@@ -1335,12 +1422,12 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
   // lib.rs:84-86 + camera.rs:66-74
   const float u = div_by_recip((float)i + gen_f32(rng), a.fw1, a.rw1);
   const float v = div_by_recip((float)j + gen_f32(rng), a.fh1, a.rh1);
-  const V3 rd = scale(rand_in_unit_disk<FROM_LDS>(rng), C.lens_radius);
+  const V3 rd = scale(rand_in_unit_disk<AB>(rng), C.lens_radius);
   const V3 off = add(scale(ld3(C.u), rd.x), scale(ld3(C.v), rd.y));
   st.ray.o = add(ld3(C.origin), off);
   st.ray.d = sub(sub(add(add(ld3(C.llc), scale(ld3(C.horizontal), u)), scale(ld3(C.vertical), v)), ld3(C.origin)),
                  off);
-  st.ray.time = gen_range<FROM_LDS>(rng, C.time0, C.time1, a.time_span);
+  st.ray.time = gen_range<AB>(rng, C.time0, C.time1, a.time_span);
   st.rng = rng;
   st.T = mk(1.f, 1.f, 1.f);
   st.depth = a.max_depth;
@@ -1376,9 +1463,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * NODE_Q; k += BLK) nodes_lds[k] = g[k];
   }
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
-  // reload a v_readlane: cornell-800 +6%, jumpy +0.8%); the mesh variants regenerate paths every ~2
-  // segments and lost 5-7% to the LDS reads' latency, so they keep the kernel arguments
-  constexpr bool SLDS = !(FEAT & F_TRI);
+  // reload a v_readlane: cornell-800 +6%, jumpy +0.8%) and in the 6 / 7-wave mesh walk (S16): at 80 VGPRs its
+  // SGPRs overflowed into VGPR lanes and 28 B per lane of scratch; with the LDS copy 12 B: monument-4k +4.5%,
+  // cow-1080p +6.7% (profiles/r05/experiments, m1).  The 5-wave mesh variants keep the kernel arguments (their
+  // paths regenerate every ~2 segments: 5-7% slower with the LDS reads in round 3).  The one-alignbit draws (AB)
+  // stay with the sphere and list-mode kernels (the triangle kernels' register allocation lost 1-2% with them).
+  constexpr bool AB = !(FEAT & F_TRI);
+  constexpr bool SLDS = AB || S16;
   __shared__ StartArgs start_lds[SLDS ? 1 : 0 + 1];
   StartArgs sa_reg;
   if constexpr (SLDS) {
@@ -1463,7 +1554,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0>(SA, id, st, stk16)) has = true;
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, id, st, stk16)) has = true;
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1545,7 +1636,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const bool iso = (FEAT & F_ISO) && mt == MT_ISOTROPIC;
       V3 rs = mk(0.f, 0.f, 0.f);
       phase(2);
-      if (lam || met || iso) rs = rand_in_unit_sphere<SLDS>(st.rng);  // vec3.rs:101-108
+      if (lam || met || iso) rs = rand_in_unit_sphere<AB>(st.rng);  // vec3.rs:101-108
       phase(3);
       const V3 ud = unit(lam ? rs : st.ray.d);                  // Lambertian: unit(rs); else unit(d_in)
       V3 att = mk(1.f, 1.f, 1.f);                                 // Dielectric: attenuation (1,1,1)
@@ -1859,6 +1950,7 @@ int upload(Scene& s, int device) {
     c.scene.uni_inst = f.uni_inst;
     c.scene.bvh_tri = f.bvh_tri;  // knob RTW_TRI_LEAF (rtw_flatten.cpp)
     c.scene.tri_inst = f.tri_inst;
+    c.scene.rect_k_small = f.rect_k_small;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
     s.dev.push_back(c);
   }

@@ -54,7 +54,7 @@ def test_render_multi_equals_render(gpu, loopback, name, aspect, w, h, spp, n):
         assert st["rays"] == st_ref["rays"], (st["rays"], st_ref["rays"])
         assert st["paths"] == w * h * spp
         dev_ms, gather_ms = many.multi_times()
-        assert len(dev_ms) == n and all(t > 0 for t in dev_ms) and gather_ms >= 0.0
+        assert len(dev_ms) == n and all(t >= 0 for t in dev_ms) and max(dev_ms) > 0 and gather_ms >= 0.0
 
 
 @pytest.mark.parametrize("n", [3, 8])
