@@ -44,6 +44,13 @@ struct alignas(16) DevPrim {
 };
 static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
 
+// A run of consecutive always-tested prims with one wrapper chain and one PrimType: the list-mode rect loop walks
+// these (no per-prim chain check or type dispatch; rtw_kernel.hip trace_rect_list)
+struct alignas(16) DevGroup {
+  uint32_t first, count, inst, type;
+};
+static_assert(sizeof(DevGroup) == 16, "DevGroup must be 16 B");
+
 struct alignas(16) DevNode {
   float b0lo[3], b0hi[3];  // child 0 box
   float b1lo[3], b1hi[3];  // child 1 box
@@ -181,11 +188,14 @@ struct DevScene {
   const uint8_t* texels;
   const DevPerlin* perlins;
   const DevShade* shade;
+  const DevGroup* lgroups;  // the always list as runs of prims of one wrapper chain and one kind, in list order
   uint32_t n_nodes, n_prims, n_always, n_insts;
+  uint32_t n_lgroups;
   uint32_t msphere_unit;  // every moving sphere's shutter is [+0, 1]: center_at needs no q2 / division
   uint32_t uni_inst;      // != 0: the scene's only instance, one Translation by uni_off
   float uni_off[3];
-  uint32_t rect_k_small;  // every rect plane has |k| < 2^62 (the list-mode rect loop's reciprocal division guard)
+  uint32_t rect_fast;     // every rect has |k| < 2^62 and ordered bounds (a0 <= a1, b0 <= b1): the list-mode rect
+                          // loop's fast path may divide by reciprocals and test bounds with med3 (trace_rect_list)
   uint32_t bvh_tri;       // every BVH leaf primitive is a triangle of instance tri_inst (the leaf fast path)
   uint32_t tri_inst;
 };

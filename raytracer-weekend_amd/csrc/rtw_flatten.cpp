@@ -719,12 +719,26 @@ int flatten(Scene& s) {
       }
     f.tshade.swap(by_prim);
   }
-  // the list-mode rect loop divides by Markstein's correction where |k - o| < 2^64 is guaranteed: |o| < 2^62
-  // per lane (checked by the kernel) and |k| < 2^62 for every rect plane (here)
-  f.rect_k_small = 1;
+  // the list-mode rect loop's fast path (rtw_kernel.hip trace_rect_list) divides by Markstein's correction, exact
+  // where |k - o| < 2^64: |o| < 2^62 per lane (checked by the kernel) and |k| < 2^62 for every rect plane (here);
+  // and it tests the bounds as med3(x, a0, a1) == x, the reference's !(x < a0 || x > a1) for finite x when
+  // a0 <= a1 (here; NaN bounds fail it too)
+  f.rect_fast = 1;
   for (const DevPrim& p : f.prims) {
     const uint32_t t = p.type_inst & 0xffu;
-    if ((t == PT_RECT_XY || t == PT_RECT_XZ || t == PT_RECT_YZ) && !(fabsf(p.q1[0]) < 0x1p62f)) f.rect_k_small = 0;
+    if ((t == PT_RECT_XY || t == PT_RECT_XZ || t == PT_RECT_YZ) &&
+        !(fabsf(p.q1[0]) < 0x1p62f && p.q0[0] <= p.q0[1] && p.q0[2] <= p.q0[3]))
+      f.rect_fast = 0;
+  }
+  // the always list as runs of one wrapper chain and one kind (DevScene::lgroups), in list order
+  for (size_t k = 0; k < f.always.size(); ++k) {
+    const DevPrim& p = f.prims[f.always[k]];
+    const uint32_t inst = p.type_inst >> 8, type = p.type_inst & 0xffu;
+    if (!f.lgroups.empty() && f.lgroups.back().inst == inst && f.lgroups.back().type == type &&
+        f.lgroups.back().first + f.lgroups.back().count == f.always[k])
+      ++f.lgroups.back().count;
+    else
+      f.lgroups.push_back(DevGroup{f.always[k], 1u, inst, type});
   }
   // spheres carry their DFS key in q1[3] too (the sphere-only kernels' 32-B test, rtw_device.hpp)
   for (DevPrim& p : f.prims) {

@@ -700,41 +700,65 @@ struct TraceState {
   bool on;       // a traversal is in progress
 };
 
-// One rect of the list-mode rect loop (rectangular.rs:27-57, :78-108, :129-159): t = (k - o_k) / d_k, the hit
-// point's two other coordinates, the bounds, and the accept (hittable/mod.rs:61-65) against the best so far.
-// `fast` (wave-uniform): the division is Markstein's correction from y_k = RN(1 / d_k), exact for the whole wave
-// (see trace_rect_list); else the IEEE division.  The list is in DFS-key order, so a later rect wins a tie: the
-// accept is t <= best.  bt starts at FLT_MAX, which also rejects t = inf and NaN.
-template <int AXIS>
-__device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, bool fast, float4 q0, float k, uint32_t pi,
-                                               float& bt, int32_t& bp) {
+// The list-mode loop of rect worlds (cornell-box: the F_BOXES | F_LIST kernel), rectangular.rs:27-57, :78-108,
+// :129-159 for every rect, hittable/mod.rs:57-69 over them.  It walks the always list as runs of one wrapper
+// chain and one kind (DevScene::lgroups): per chain the object-space ray, per run one specialised loop, so a rect
+// costs no chain check and no type dispatch -- the scalar unit, which one CU's four SIMDs share, had become the
+// limit of this loop (~35 SALU per rect against 17 VALU, profiles/r05/experiments).
+// Fast path (wave-uniform, per chain): the division (k - o_k) / d_k is Markstein's correction from
+// y_k = RN(1 / d_k) (rcp_rn_fast, exact in [2^-126, 2^126]; 3 VALU instead of the IEEE division's 11), the IEEE
+// quotient whenever |d_k| is in [2^-60, 2^60] and |k - o_k| < 2^64 (|k| < 2^62 for every rect, DevScene::rect_fast;
+// |o_k| < 2^62 per lane): then nothing over- or underflows unless |quotient| < 2^-42, where both are < TMIN and
+// rejected alike (Markstein 1990; div_by_recip).  There t, the hit point's x, y are finite or +-inf, and the
+// reference's tests `t >= TMIN`, `t <= best` and `!(x < a0 || x > a1)` are med3(v, lo, hi) == v (lo <= hi holds:
+// TMIN <= best always, a0 <= a1 for every rect, DevScene::rect_fast): 3 med3 + 3 compares and 2 scalar ands instead
+// of 6 compares and 5.  A chain where any lane of the wave is outside that range runs the reference's IEEE
+// division and compares (slow path).  The list is in DFS-key order, so a later rect wins a tie: accept t <= best
+// (no key compare; bt starts at FLT_MAX, which also rejects t = inf).  VERDICT r4 item 3.
+template <int AXIS, bool FAST>
+__device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, float4 q0, float k, uint32_t pi, float& bt,
+                                               int32_t& bp) {
   const float o_k = AXIS == 0 ? lr.o.z : (AXIS == 1 ? lr.o.y : lr.o.x);
   const float d_k = AXIS == 0 ? lr.d.z : (AXIS == 1 ? lr.d.y : lr.d.x);
   const float y_k = AXIS == 0 ? y.z : (AXIS == 1 ? y.y : y.x);
   const float o_a = AXIS == 2 ? lr.o.y : lr.o.x, d_a = AXIS == 2 ? lr.d.y : lr.d.x;
   const float o_b = AXIS == 0 ? lr.o.y : lr.o.z, d_b = AXIS == 0 ? lr.d.y : lr.d.z;
   const float num = k - o_k;
-  float t;
-  if (fast) t = div_by_recip(num, d_k, y_k);
-  else t = num / d_k;
-  const float x = o_a + t * d_a;
-  const float yy = o_b + t * d_b;
-  const bool out = (x < q0.x) | (x > q0.y) | (yy < q0.z) | (yy > q0.w);
-  const bool acc = (t >= TMIN) & (t <= bt) & !out;
-  bt = acc ? t : bt;
+  bool acc;
+  if constexpr (FAST) {
+    const float t = div_by_recip(num, d_k, y_k);
+    const float x = o_a + t * d_a;
+    const float yy = o_b + t * d_b;
+    acc = (__builtin_amdgcn_fmed3f(t, TMIN, bt) == t) & (__builtin_amdgcn_fmed3f(x, q0.x, q0.y) == x) &
+          (__builtin_amdgcn_fmed3f(yy, q0.z, q0.w) == yy);
+    bt = acc ? t : bt;
+  } else {
+    const float t = num / d_k;
+    const float x = o_a + t * d_a;
+    const float yy = o_b + t * d_b;
+    const bool out = (x < q0.x) | (x > q0.y) | (yy < q0.z) | (yy > q0.w);
+    acc = (t >= TMIN) & (t <= bt) & !out;
+    bt = acc ? t : bt;
+  }
   bp = acc ? (int32_t)pi : bp;
 }
 
-// The list-mode loop of rect worlds (cornell-box: the F_BOXES | F_LIST kernel).  Per wrapper chain (a Cuboid's
-// six sides are adjacent) the object-space ray and the reciprocals y = RN(1 / d) of its three direction
-// components (rcp_rn_fast: exact in [2^-126, 2^126]); each rect's division (k - o_k) / d_k is then Markstein's
-// correction from y_k (3 VALU) instead of the IEEE division (11).  It is the IEEE quotient whenever
-// |d_k| in [2^-60, 2^60] and |k - o_k| < 2^64 (|k| < 2^62 for every rect: DevScene::rect_k_small; |o_k| < 2^62
-// per lane): then no step over- or underflows unless |quotient| < 2^-42, where both are < TMIN and rejected
-// alike (Markstein 1990; div_by_recip).  A chain where any lane of the wave is outside that range takes the IEEE
-// division for the whole wave (a scalar branch, no per-rect exec masking).
-// The rect test's bounds and the accept are one set of compares and two selects (the key is not needed: the
-// list is in DFS-key order).  VERDICT r4 item 3.
+// one run of rects of one kind (AXIS) and chain: the whole 64-B record in one scalar load (s_load_dwordx16)
+template <bool COUNT, int AXIS, bool FAST>
+__device__ __forceinline__ void rect_list_run(const DevScene& S, uint32_t first, uint32_t count, const Ray& lr, V3 y,
+                                              float& bt, int32_t& bp, uint32_t* cnt) {
+  typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+  const __attribute__((address_space(4))) u16v* P = (const __attribute__((address_space(4))) u16v*)(S.prims + first);
+#pragma unroll 2
+  for (uint32_t k = 0; k < count; ++k) {
+    const u16v rec = P[k];
+    const float4 q0 = make_float4(__uint_as_float(rec[0]), __uint_as_float(rec[1]), __uint_as_float(rec[2]),
+                                  __uint_as_float(rec[3]));
+    rect_list_test<AXIS, FAST>(lr, y, q0, __uint_as_float(rec[4]), first + k, bt, bp);
+    if (COUNT) { cnt[1]++; cnt[2 + PT_RECT_XY + AXIS]++; simd_tick(cnt, 10, 11); }
+  }
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r, Best& best, uint32_t* cnt) {
   float bt = 0x1.fffffep127f;  // FLT_MAX
@@ -743,41 +767,25 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
   Ray lr = r;
   V3 y = mk(0.f, 0.f, 0.f);
   bool fast = false;
-  const uint32_t a0 = S.n_prims - S.n_always;  // the always-tested prims are the table's last (rtw_flatten.cpp)
-  // the whole 64-B record in one scalar load (s_load_dwordx16): one round trip per rect
-  typedef uint32_t u16v __attribute__((ext_vector_type(16)));
-  auto ld_rec = [&](uint32_t pi) -> u16v { return *(const __attribute__((address_space(4))) u16v*)(S.prims + pi); };
-#ifndef RTW_RECT_PIPE
-#define RTW_RECT_PIPE 0
-#endif
-  u16v nxt;
-  if (RTW_RECT_PIPE && S.n_always) nxt = ld_rec(a0);
-  for (uint32_t k = 0; k < S.n_always; ++k) {
-    const uint32_t pi = a0 + k;
-    u16v rec;
-    if (RTW_RECT_PIPE) {  // (experiment) the next rect's record loads while this one is tested
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this rect's record (and nothing else) has arrived
-      rec = nxt;
-      nxt = ld_rec(min(pi + 1u, S.n_prims - 1u));
-    } else {
-      rec = ld_rec(pi);
-    }
-    const float4 q0 = make_float4(__uint_as_float(rec[0]), __uint_as_float(rec[1]), __uint_as_float(rec[2]),
-                                  __uint_as_float(rec[3]));
-    const float4 q1 = make_float4(__uint_as_float(rec[4]), 0.f, 0.f, 0.f);
-    const uint32_t inst = rec[12] >> 8, type = rec[12] & 0xffu;
-    if (inst != cur) {  // wave-uniform
-      cur = inst;
-      lr = inst ? to_local<true>(S.insts + inst, r) : r;
+  for (uint32_t g = 0; g < S.n_lgroups; ++g) {
+    const uint4 G = uload(reinterpret_cast<const uint4*>(S.lgroups + g));  // (first, count, instance, kind)
+    if (G.z != cur) {  // wave-uniform
+      cur = G.z;
+      lr = cur ? to_local<true>(S.insts + cur, r) : r;
       y = mk(rcp_rn_fast(lr.d.x), rcp_rn_fast(lr.d.y), rcp_rn_fast(lr.d.z));
       const bool ok = recip_div_ok(lr.d.x) && recip_div_ok(lr.d.y) && recip_div_ok(lr.d.z) &&
                       fabsf(lr.o.x) < 0x1p62f && fabsf(lr.o.y) < 0x1p62f && fabsf(lr.o.z) < 0x1p62f;
-      fast = S.rect_k_small && __ballot(!ok) == 0;
+      fast = S.rect_fast && __ballot(!ok) == 0;
     }
-    if (type == PT_RECT_XY) rect_list_test<0>(lr, y, fast, q0, q1.x, pi, bt, bp);
-    else if (type == PT_RECT_XZ) rect_list_test<1>(lr, y, fast, q0, q1.x, pi, bt, bp);
-    else rect_list_test<2>(lr, y, fast, q0, q1.x, pi, bt, bp);
-    if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }
+    if (fast) {
+      if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      else if (G.w == PT_RECT_XZ) rect_list_run<COUNT, 1, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      else rect_list_run<COUNT, 2, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
+    } else {
+      if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      else if (G.w == PT_RECT_XZ) rect_list_run<COUNT, 1, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      else rect_list_run<COUNT, 2, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
+    }
   }
   best.t = bt;
   best.prim = bp;
@@ -1846,12 +1854,13 @@ static Variant pick5(uint32_t need, bool half = false, bool codes16 = false) {
     // 16-bit stack entries (the nodes' codes: half the LDS of the 32-bit stack, whose 31 KB per workgroup allow
     // 5 per CU) and the paths' T / depth / id in LDS state rows, at 6 or 7 waves / SIMD (knob RTW_MESH_S16; 0 =
     // the 32-bit stack at 5).  Measured (r04n, r04p): monument-4k +3.0% at 6 waves (80 VGPRs), +2.2% more with
-    // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows, so by default
-    // the half-node trees (>= 2048 node4s) take it and the smaller f32-node trees keep the 5-wave kernel.
-    int s16 = env_int("RTW_MESH_S16", half ? 6 : 0);
+    // the state rows (scratch 40 -> 32 B), 7 waves slower; cow-1080p -4.1% / -0.7% with the rows.  With the
+    // start_path operands in LDS (round 5, m1) the SGPR overflow is gone and 7 waves (72 VGPRs) win: monument
+    // +2.3%, cow +0.8% over 6 (profiles/r05/experiments, m2), so every tree with half nodes takes the 7-wave walk.
+    int s16 = env_int("RTW_MESH_S16", half ? 7 : 0);
     if (s16 != 0 && s16 != 6 && s16 != 7) {  //  no silent fallback for a value no variant has
       fprintf(stderr, "rtw: RTW_MESH_S16=%d ignored (0, 6 or 7)\n", s16);
-      s16 = half ? 6 : 0;
+      s16 = half ? 7 : 0;
     }
     if (codes16 && s16 != 0 && need <= (uint32_t)STACK_DEEP5) {
       const uint32_t st = (uint32_t)STACK_DEEP5;
@@ -1911,7 +1920,7 @@ int upload(Scene& s, int device) {
   size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
-  size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h);
+  size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h), o_groups = put(blob, f.lgroups);
   blob.resize((blob.size() + 255) & ~(size_t)255);
   int d0 = device >= 0 ? device : 0, d1 = device >= 0 ? device + 1 : nlog;
   int prev = 0;
@@ -1942,6 +1951,8 @@ int upload(Scene& s, int device) {
     c.scene.texels = (const uint8_t*)(base + o_texel);
     c.scene.perlins = (const DevPerlin*)(base + o_perlin);
     c.scene.shade = (const DevShade*)(base + o_shade);
+    c.scene.lgroups = (const DevGroup*)(base + o_groups);
+    c.scene.n_lgroups = (uint32_t)f.lgroups.size();
     c.scene.n_nodes = (uint32_t)f.nodes4.size();
     c.scene.n_prims = (uint32_t)f.prims.size();
     c.scene.n_always = (uint32_t)f.always.size();
@@ -1950,7 +1961,7 @@ int upload(Scene& s, int device) {
     c.scene.uni_inst = f.uni_inst;
     c.scene.bvh_tri = f.bvh_tri;  // knob RTW_TRI_LEAF (rtw_flatten.cpp)
     c.scene.tri_inst = f.tri_inst;
-    c.scene.rect_k_small = f.rect_k_small;
+    c.scene.rect_fast = f.rect_fast;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
     s.dev.push_back(c);
   }

@@ -74,7 +74,8 @@ struct Flat {
   uint32_t features = 0;  // Feature bits actually used
   uint32_t msphere_unit = 1;  // every moving sphere has the shutter [+0, 1] (DevPrim::aux)
   uint32_t uni_inst = 0;      // the only instance, a single Translation (0 = none such)
-  uint32_t rect_k_small = 0;  // every rect plane |k| < 2^62 (DevScene::rect_k_small)
+  uint32_t rect_fast = 0;     // DevScene::rect_fast
+  std::vector<DevGroup> lgroups;  // DevScene::lgroups
   uint32_t bvh_tri = 0;       // every BVH leaf is a triangle of wrapper chain tri_inst (DevScene::bvh_tri)
   uint32_t tri_inst = 0;
   float uni_off[3] = {0, 0, 0};

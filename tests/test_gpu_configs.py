@@ -112,9 +112,10 @@ def test_corrupt_bvh_fails_every_path(gpu, knobs, knob):
 def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, knobs, knob):
     """after a guard trip the kernel closes the path queue and empties the wave's id pool, so a
     large corrupt frame costs about one trip per wave, not one per 64 paths.  A 256x256x16 frame (16 K
-    64-path groups, ~1 K waves with work) must take at most 8x the time of an 8x8x1 frame (one wave, one
-    trip); without the drain every wave runs ~16 trips in a row."""
-    import time
+    64-path groups, ~1 K waves with work) must take at most 8x the path-kernel time of an 8x8x1 frame (one
+    wave, one trip); without the drain every wave runs ~16 trips in a row.  A smoke check on device time (the
+    library's HIP events around the launch, rtw_path_kernel_times, read after rtw_render_status has reported and
+    cleared the fault), not on host wall clock."""
     torch = pytest.importorskip("torch")
     if knob:
         knobs.setenv(*knob.split("="))
@@ -128,19 +129,20 @@ def test_corrupt_bvh_frame_drains_after_one_trip_per_wave(gpu, knobs, knob):
         out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
         rt = rtw.Raytracer(s, cam, bg, w, h, spp, seed=1)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        s.path_kernel_times(0)  # forget earlier launches
         rt.render_device(out.data_ptr(), 0, 0, 0, stream)
         torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
         with pytest.raises(rtw.RtwError):
-            s.render_status(0)
-        return dt
+            s.render_status(0)  # reports the fault and clears it
+        t = s.path_kernel_times(0)
+        assert len(t) == 1
+        return t[0]
 
     timed(8, 8, 1)  # warm-up (buffers, code objects)
     small = timed(8, 8, 1)
     big = timed(256, 256, 16)
-    print(f"corrupt frames: 8x8x1 {small:.3f} s, 256x256x16 {big:.3f} s")
-    assert big <= 8.0 * small + 0.5, (small, big)
+    print(f"corrupt frames, path-kernel ms: 8x8x1 {small:.3f}, 256x256x16 {big:.3f}")
+    assert big <= 8.0 * small + 5.0, (small, big)
 
 
 def test_render_multi_one_gpu_needs_no_rccl(gpu, monkeypatch):
