@@ -825,10 +825,16 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     for (uint32_t k = 0; k < S.n_always; ++k)
       test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
   }
-  // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR
-  // across the whole loop and spilled it
+  // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR across the
+  // whole loop and spilled it.  Triangle kernels (the mesh walk): as a scalar, since the 7-wave walk spilled even
+  // the opaque VGPR copy to scratch (one reload per segment; s1)
   int32_t root = S.n_nodes ? 0 : -1;
-  asm volatile("" : "+v"(root));
+  if constexpr ((FEAT & F_TRI) != 0) {
+    root = __builtin_amdgcn_readfirstlane(root);
+    asm volatile("" : "+s"(root));
+  } else {
+    asm volatile("" : "+v"(root));
+  }
   ts.node = root;
   ts.pend = 0;
   ts.sp = 0;
@@ -1514,7 +1520,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
   // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
   __shared__ uint64_t pool_lds[BLK / 64][3];
-  uint64_t* const pool = pool_lds[threadIdx.x >> 6];
+  // S16 mesh walk: the wave index as a scalar, so the pool address is rebuilt from an SGPR (one v_mov) where it is
+  // used instead of kept in a VGPR (the 7-wave walk spilled it to scratch and reloaded it at every regeneration;
+  // the sphere and list-mode kernels measured 0.5-1.4% slower with it, profiles/r05/experiments s1)
+  uint64_t* const pool = pool_lds[S16 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
   bool exhausted = false;                // wave-uniform
   bool has = false;
@@ -1603,9 +1612,15 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     const Best b = ts.b;
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
-    const V3 T = LST ? mk(__uint_as_float(lst_ld(0)), __uint_as_float(lst_ld(1)), __uint_as_float(lst_ld(2))) : st.T;
+    // the throughput; the S16 mesh walk reads it from its LDS rows where it is used, after the hit record and the
+    // material, so it is not held across them (the 7-wave walk had spilled T.z to scratch there; s1)
+    const V3 T0 = (LST && !S16) ? mk(__uint_as_float(lst_ld(0)), __uint_as_float(lst_ld(1)), __uint_as_float(lst_ld(2)))
+                                : st.T;
+    auto path_T = [&]() -> V3 {
+      return (LST && S16) ? mk(__uint_as_float(lst_ld(0)), __uint_as_float(lst_ld(1)), __uint_as_float(lst_ld(2))) : T0;
+    };
     if (b.prim < 0) {  // lib.rs:102-105
-      L = mul(T, bg);
+      L = mul(path_T(), bg);
       done = true;
       if (__builtin_expect(b.prim == -2, 0)) {
         // trace_run tripped its guard (a corrupt tree; the frame is invalid and reported): close the path queue
@@ -1660,7 +1675,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         else if (FEAT & F_TEXGEN) att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
       }
       if (light) {  // emit, no scatter
-        L = mul(T, att);
+        L = mul(path_T(), att);
         done = true;
       } else {
         V3 dir = rs;  // Isotropic (material.rs:155-165): never absorbs
@@ -1681,7 +1696,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           if (cannot || reflectance(cos_t, r0) > gen_f32(st.rng)) dir = reflect(ud, h.n);
           else dir = refract(ud, h.n, ratio);
         }
-        const V3 T2 = mul(T, att);  // x * 1.0f == x: the Dielectric's T is unchanged
+        const V3 T2 = mul(path_T(), att);  // x * 1.0f == x: the Dielectric's T is unchanged
         if constexpr (LST) {
           lst_st(0, __float_as_uint(T2.x));
           lst_st(1, __float_as_uint(T2.y));
