@@ -749,14 +749,19 @@ __device__ __forceinline__ void rect_list_run(const DevScene& S, uint32_t first,
                                               float& bt, int32_t& bp, uint32_t* cnt) {
   typedef uint32_t u16v __attribute__((ext_vector_type(16)));
   const __attribute__((address_space(4))) u16v* P = (const __attribute__((address_space(4))) u16v*)(S.prims + first);
-#pragma unroll 2
-  for (uint32_t k = 0; k < count; ++k) {
+  auto one = [&](uint32_t k) {
     const u16v rec = P[k];
     const float4 q0 = make_float4(__uint_as_float(rec[0]), __uint_as_float(rec[1]), __uint_as_float(rec[2]),
                                   __uint_as_float(rec[3]));
     rect_list_test<AXIS, FAST>(lr, y, q0, __uint_as_float(rec[4]), first + k, bt, bp);
     if (COUNT) { cnt[1]++; cnt[2 + PT_RECT_XY + AXIS]++; simd_tick(cnt, 10, 11); }
+  };
+  uint32_t k = 0;
+  for (; k + 1u < count; k += 2u) {  // two rects per trip (a Cuboid's runs are pairs)
+    one(k);
+    one(k + 1u);
   }
+  if (k < count) one(k);
 }
 
 template <bool COUNT>
@@ -1172,8 +1177,39 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   const DevInst* I = S.insts + inst;
   const bool uni = (FEAT & F_INST) && inst && inst == S.uni_inst;  // one Translation, offset uniform
   Ray lr = wr;
-  if (uni) lr.o = sub(wr.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
-  else if ((FEAT & F_INST) && inst) lr = to_local(I, wr);
+  // Chains of at most two wrappers (a Cuboid's .rotate_y().translate(): cornell-box, the book-2 scenes), in the
+  // kernels without triangles: the header and both ops in three independent loads and the directions after each op
+  // kept for the unwinding below, instead of the generic loops' chain of dependent loads and per-level recomputation
+  // (the same f32 operations).
+  bool short_chain = false;
+  uint32_t nops = 0;
+  float4 op0 = make_float4(0.f, 0.f, 0.f, 0.f), op1 = op0;
+  V3 d0 = wr.d, d1 = wr.d;  // the ray direction inside wrapper 0 (after op 0) and wrapper 1 (after ops 0, 1)
+  auto apply_op = [](float4 op, Ray& r) {  // transformations.rs:23-28 / :115-135, as to_local
+    if (op.x == (float)IO_TRANSLATE) {
+      r.o = sub(r.o, mk(op.y, op.z, op.w));
+    } else {
+      const float s = op.y, c = op.z;
+      r.o = mk(c * r.o.x - s * r.o.z, r.o.y, s * r.o.x + c * r.o.z);
+      r.d = mk(c * r.d.x - s * r.d.z, r.d.y, s * r.d.x + c * r.d.z);
+    }
+  };
+  if (uni) {
+    lr.o = sub(wr.o, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
+  } else if ((FEAT & F_INST) && inst) {
+    nops = I->nops;
+    op0 = *reinterpret_cast<const float4*>(I->op[0]);
+    op1 = *reinterpret_cast<const float4*>(I->op[1]);
+    short_chain = !(FEAT & F_TRI) && nops <= 2u;  // (the mesh kernels' registers are spoken for: generic path)
+    if (short_chain) {
+      apply_op(op0, lr);
+      d0 = lr.d;
+      if (nops == 2u) apply_op(op1, lr);
+      d1 = lr.d;
+    } else {
+      lr = to_local(I, wr);
+    }
+  }
   const float t = b.t;
   Rec h;
   h.mat = meta.z;
@@ -1217,6 +1253,21 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   if (uni) {  // transformations.rs:29-37: p + offset, face normal against the world ray
     h.p = add(h.p, mk(S.uni_off[0], S.uni_off[1], S.uni_off[2]));
     face(h, wr.d, h.n);
+  } else if ((FEAT & F_INST) && inst && short_chain) {  // unwind inner -> outer (transformations.rs:29-37, :137-147)
+    auto unwind_op = [&](float4 op, V3 dk) {
+      if (op.x == (float)IO_TRANSLATE) {
+        h.p = add(h.p, mk(op.y, op.z, op.w));
+        face(h, dk, h.n);
+      } else {
+        const float s = op.y, c = op.z;
+        V3 p = mk(c * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + c * h.p.z);
+        V3 n = mk(c * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + c * h.n.z);
+        h.p = p;
+        face(h, dk, n);
+      }
+    };
+    if (nops == 2u) unwind_op(op1, d1);
+    if (nops >= 1u) unwind_op(op0, d0);
   } else if ((FEAT & F_INST) && inst) {  // unwind wrappers inner -> outer (transformations.rs:29-37, :137-147)
     for (int k = (int)I->nops - 1; k >= 0; --k) {
       V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
