@@ -335,8 +335,10 @@ int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32
 /* 0 leaf primitives, 1 materials, 2 textures, 3 BVH nodes, 4 BVH depth, 5 always-tested
  * primitives, 6 instances, 7 BVH2 nodes, 8 traversal-stack bound, 9 feature mask (rtw_device.hpp
  * Feature; selects the path-kernel variant), 10 Perlin tables, 11 stack bound of the sorted-push
- * walk (LDS-node kernels).  7-9 and 11 are valid once rtw_scene_commit has flattened
- * the scene (also when its upload failed for lack of a device). */
+ * walk (LDS-node kernels), 12 runs of the always list (one wrapper chain and one prim kind each: the
+ * list-mode rect loop's program), 13 1 if every rect admits the list loop's fast path (|k| < 2^62,
+ * ordered bounds).  3-13 are valid once rtw_scene_commit has flattened the scene (also when its upload
+ * failed for lack of a device). */
 int64_t rtw_scene_info(const rtw_scene* s, int what);
 /* Introspection for the test harness: the flattened 4-wide BVH (DevNode4, 128 B each, breadth-first
  * numbered; csrc/rtw_device.hpp), valid once rtw_scene_commit has flattened the scene (also when its

@@ -587,6 +587,8 @@ int64_t rtw_scene_info(const rtw_scene* s, int what) {
     case 9: return (int64_t)sc.flat.features;
     case 10: return (int64_t)sc.flat.perlins.size();
     case 11: return (int64_t)sc.flat.stack_need4;
+    case 12: return (int64_t)sc.flat.lgroups.size();
+    case 13: return (int64_t)sc.flat.rect_fast;
     case 4: return (int64_t)sc.flat.depth;
     case 5: return (int64_t)sc.flat.always.size();
     case 6: return (int64_t)sc.flat.insts.size();

@@ -306,3 +306,21 @@ def test_alias_devices_arguments(rtw):
         assert e.value.code == rtw.RTW_EINVAL
     s.diag_alias_devices(8)
     s.diag_alias_devices(2)  # may be changed until the commit
+
+
+def test_list_runs_and_rect_fast_flag(rtw):
+    """The list-mode rect loop's program (DevScene::lgroups, rtw_scene_info 12): cornell-box's 18 always-tested
+    rects form 9 runs of one wrapper chain and one kind, in list order (the room's yz yz | xz xz xz | xy, then
+    each box's xy | xz | yz pairs); its fast path (info 13) needs |k| < 2^62 and ordered bounds on every rect,
+    which a plane at 1e19 or an inverted rect revokes."""
+    s = rtw.Scene()
+    s.preset("cornell-box", 1.0, seed=3)
+    _commit_anywhere(rtw, s)
+    assert (s.info(5), s.info(12), s.info(13)) == (18, 9, 1)
+    for k, bounds in ((1e19, (0.0, 1.0, 0.0, 1.0)), (1.0, (1.0, 0.0, 0.0, 1.0))):
+        s = rtw.Scene()
+        m = s.lambertian_solid((0.5, 0.5, 0.5))
+        s.xy_rect(0.0, 1.0, 0.0, 1.0, 0.0, m)
+        s.xy_rect(bounds[0], bounds[1], bounds[2], bounds[3], k, m)
+        _commit_anywhere(rtw, s)
+        assert s.info(5) == 2 and s.info(12) == 1 and s.info(13) == 0
