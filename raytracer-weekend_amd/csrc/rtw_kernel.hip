@@ -46,13 +46,17 @@ namespace dev {
 
 // Compile-time switches.  The product build sets none of them.  Only these remain, and none changes a
 // result: RTW_NT_SAMPLES (0 = the sample buffer written / read with plain accesses; an A/B knob) and the
-// COUNT-build lane diagnostics RTW_LANE_DIAG / RTW_UNI_DIAG.  RTW_DIAG_ONE_TRIP (a timing diagnostic that is
+// COUNT-build diagnostics RTW_LANE_DIAG / RTW_UNI_DIAG (node-loop lane states) and RTW_SHADE_DIAG (shading
+// sub-phase timers; each replaces the COUNT build's sub_cycles).  RTW_DIAG_ONE_TRIP (a timing diagnostic that is
 // NOT the reference's distribution) refuses to compile unless RTW_ALLOW_NON_REFERENCE is set as well, so no
 // product build can carry it.  Round 3's equivalence switches (sphere-root / unit() reciprocals, the
 // precomputed Dielectric ratios, start_path's LDS operands, select-form rect tests) are the only code now;
-// the dropped experiments (per-chain rect reciprocals, the xoroshiro64+ output) are deleted.
+// the dropped experiments (round 3's per-rect-guarded chain reciprocals, the xoroshiro64+ output) are deleted.
 #if defined(RTW_DIAG_ONE_TRIP) && !defined(RTW_ALLOW_NON_REFERENCE)
 #error "RTW_DIAG_ONE_TRIP changes the sampled distribution (not the reference's): diagnostic builds only"
+#endif
+#if defined(RTW_DIAG_NO_STORE) && !defined(RTW_ALLOW_NON_REFERENCE)
+#error "RTW_DIAG_NO_STORE drops the sample stores (the image is not computed): diagnostic builds only"
 #endif
 #if defined(RTW_RNG_PLUS) || defined(RTW_RECT_RCP) || defined(RTW_SPH_RCP) || defined(RTW_FAST_RCP) || \
     defined(RTW_DIEL_PRE) || defined(RTW_START_LDS) || defined(RTW_RECT_SELECT)
@@ -1700,6 +1704,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       Rec h;
       if (!solid_light) h = hit_record<FEAT>(S, st.ray, b, sh.kind);
       else h = Rec{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.0f, 0.0f, true, 0u};
+#ifdef RTW_SHADE_DIAG  // COUNT-build diagnostic: shading sub-phases (hit record, unit + texture, scatter) in ph[7..9]
+      phase(7);
+#endif
       // One body for every material (material.rs:42-165, light_source.rs:17-24): a wave mixing
       // materials runs the rejection loop, unit() and the texture lookup once instead of once per
       // material branch.  Each material's draws and f32 operations are unchanged.
@@ -1725,6 +1732,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           att = image_texel(S, __float_as_uint(sh.a[0]), __float_as_uint(sh.a[1]), __float_as_uint(sh.a[2]), h.u, h.v);
         else if (FEAT & F_TEXGEN) att = tex_value<FEAT>(S, S.mats[h.mat].tex, h.u, h.v, h.p);
       }
+#ifdef RTW_SHADE_DIAG
+      phase(8);
+#endif
       if (light) {  // emit, no scatter
         L = mul(path_T(), att);
         done = true;
@@ -1758,6 +1768,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         st.ray.o = h.p;
         st.ray.d = dir;
       }
+#ifdef RTW_SHADE_DIAG
+      phase(9);
+#endif
       if (!done) {  // lib.rs:98-100: depth 0 returns black
         if constexpr (LST) {
           const uint32_t d = lst_ld(3) - 1u;
@@ -1770,6 +1783,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     }
     if (done) {
       float* o = a.sbuf + (size_t)(LST ? lst_ld(4) : st.pid) * 3u;  // one path's 12 B share a cache line
+#ifdef RTW_DIAG_NO_STORE  // timing diagnostic only: what the sample stores (and the waits behind them) cost
+      if (L.x == -1.2345f) o[0] = L.y;  // (keeps L live; never true for a finite non-negative radiance)
+#else
 #if RTW_NT_SAMPLES
       // streaming stores: the 12.7 GB of samples per frame should not evict the scene tables and the
       // register spill lines from L2 (they are read back once, by reduce_kernel)
@@ -1781,6 +1797,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       o[1] = L.y;
       o[2] = L.z;
 #endif
+#endif  // RTW_DIAG_NO_STORE
       has = false;
     }
   }
@@ -1790,7 +1807,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     if (lane == 0) {
       for (int k = 0; k < 3; ++k) atomicAdd(a.counters + 16 + k, (unsigned long long)ph[k]);
       atomicAdd(a.counters + 19, (unsigned long long)(t_mark - t_start));
-#if defined(RTW_LANE_DIAG) || defined(RTW_UNI_DIAG)
+#if defined(RTW_LANE_DIAG) || defined(RTW_UNI_DIAG) || defined(RTW_SHADE_DIAG)
       for (int k = 7; k < 11; ++k) atomicAdd(a.counters + 13 + k, (unsigned long long)ph[k]);
 #else
       for (int k = 3; k < 7; ++k) atomicAdd(a.counters + 17 + k, (unsigned long long)ph[k]);
