@@ -1,7 +1,7 @@
 """a build cannot carry a parity-breaking or removed compile-time switch.
 
 rtw_kernel.hip refuses (#error) RTW_DIAG_ONE_TRIP (a timing diagnostic that samples the cube, not the
-reference's unit ball) unless RTW_ALLOW_NON_REFERENCE is set too, and every switch round 4 removed (the
+reference's unit ball) and RTW_DIAG_NO_STORE (one that drops the sample stores) unless RTW_ALLOW_NON_REFERENCE is set too, and every switch round 4 removed (the
 xoroshiro64+ output RTW_RNG_PLUS, the dropped reciprocal rect test RTW_RECT_RCP, the folded equivalence
 switches).  Preprocessing is enough to see the #error, so no device compile runs here."""
 import shutil
@@ -29,7 +29,7 @@ def test_product_build_preprocesses():
     assert r.returncode == 0, r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("macro", ["RTW_DIAG_ONE_TRIP", "RTW_RNG_PLUS", "RTW_RECT_RCP=1", "RTW_SPH_RCP=0",
+@pytest.mark.parametrize("macro", ["RTW_DIAG_ONE_TRIP", "RTW_DIAG_NO_STORE", "RTW_RNG_PLUS", "RTW_RECT_RCP=1", "RTW_SPH_RCP=0",
                                    "RTW_FAST_RCP=0", "RTW_DIEL_PRE=0", "RTW_START_LDS=0", "RTW_RECT_SELECT=0"])
 def test_parity_breaking_or_removed_switch_fails_the_build(macro):
     r = _preprocess(macro)
@@ -37,5 +37,6 @@ def test_parity_breaking_or_removed_switch_fails_the_build(macro):
     assert "#error" in r.stderr or "error:" in r.stderr
 
 
-def test_diagnostic_build_needs_explicit_opt_in():
-    assert _preprocess("RTW_DIAG_ONE_TRIP", "RTW_ALLOW_NON_REFERENCE").returncode == 0
+@pytest.mark.parametrize("macro", ["RTW_DIAG_ONE_TRIP", "RTW_DIAG_NO_STORE"])
+def test_diagnostic_build_needs_explicit_opt_in(macro):
+    assert _preprocess(macro, "RTW_ALLOW_NON_REFERENCE").returncode == 0
