@@ -2335,6 +2335,16 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
     a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
     const int grid = resident_grid(c, fn, var.block, count);
+    // Small frames: fewer ids per atomic, halving until every resident wave can take >= 32 batches.  configs[0]
+    // (jumpy-balls 400x225x50: 4.5 M paths for 8,192 resident waves) handed out 4,395 batches of 1,024, so half the
+    // waves got none and the kernel ran 5x slower per ray than at 1080p: 5.43k -> 9.30k Mrays/s at 128.  The same
+    // for an 8-GPU share (one eighth of the paths): jumpy +5% at 256, cornell +4.4% at 256, cow +22% at 512
+    // (profiles/r05/experiments, r05l).  Floors: the mesh / generic kernels' short paths queue on the one atomic
+    // word below 512 (cow 256: -16%), the others' below 128.  Full frames keep the defaults (>= 32 batches per
+    // wave already); knob RTW_BATCH sets the size outright.
+    const uint32_t batch0 = a.batch, batch_floor = batch0 >= 2048u ? 512u : 128u;
+    const bool batch_auto = tuning_env("RTW_BATCH") == nullptr;
+    const uint64_t waves = (uint64_t)grid * var.block / 64u;
     // the LDS-node variants walk 16-bit codes within their own stack rows (pick_kernel checked
     // stack_need4 against them) and have no HBM spill path
     const uint32_t lds = var.stack;
@@ -2353,6 +2363,9 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
       a.n_paths = (uint64_t)ns * per_slot;
+      a.batch = batch0;
+      if (batch_auto)
+        while (a.batch / 2u >= batch_floor && a.n_paths < (uint64_t)a.batch * waves * 32u) a.batch /= 2u;
       if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
       hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
