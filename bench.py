@@ -16,8 +16,11 @@ hot path, with the scene already resident in HBM.  On one GPU the frame renders 
 the device image (rtw_render_device without tile ids, rtw_render's path).  On N GPUs the frame's
 8x8 tiles are dealt round-robin to the N ranks (one process per GPU, rtw_tile_partition); each
 rank renders its tiles with rtw_render_device, then one RCCL all-gather over xGMI brings every
-rank's packed tiles to all ranks and rank 0 unpacks the framebuffer.  Rank 0 copies the frame
-to the host inside the timed step.  Total work
+rank's packed tiles to all ranks and rank 0 unpacks the framebuffer.  The step ends with the frame
+in rank 0's HBM (the C-ABI's rtw_render_device output); the rate with rank 0 also copying it to pinned
+host memory in every step (rtw_render's host-buffer boundary, over PCIe) is timed separately and printed
+as `pcie_inclusive` -- never `value` (the single-process --multi-device path returns a host frame from
+rtw_render_multi, so there the two are the same).  Total work
 is fixed as N grows ("scaling": "strong").  value = rays of the frame (world.hit queries,
 lib.rs:102, counted exactly by the kernel) / max-over-ranks step time.
 
@@ -299,7 +302,7 @@ def main() -> int:
             a, b = int(bounds[k]), int(bounds[k + 1])
             rt.render_device(packed[a:].data_ptr(), dev, ids[a:].data_ptr(), b - a, stream.cuda_stream)
 
-    def frame_end():
+    def frame_end(to_host):
         if multi:
             return
         if world > 1 and args.backend == "gloo":  # CPU rehearsal: gather through host memory
@@ -327,7 +330,7 @@ def main() -> int:
         elif launches > 1:
             rtw.unpack_tiles_device(w, h, ids.data_ptr(), n_mine, packed.data_ptr(), image.data_ptr(), dev,
                                     stream.cuda_stream)
-        if rank == 0:
+        if rank == 0 and to_host:
             host_image.copy_(image, non_blocking=True)
 
     gev = None         # (start, end) events of the current step's all-gather (N > 1)
@@ -351,10 +354,10 @@ def main() -> int:
 
     for _ in range(args.warmup):
         render_frame()
-        frame_end()
+        frame_end(True)
     if args.check_image:  # the gathered frame must equal a single-device render, bit for bit
         render_frame()
-        frame_end()
+        frame_end(False)
         torch.cuda.synchronize()
         if rank == 0:
             ref = torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
@@ -376,21 +379,31 @@ def main() -> int:
     torch.cuda.synchronize()
     if multi:
         timing_multi = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+
+    def timed(to_host, events):  # K steps between barriers + synchronize, max over ranks
+        nonlocal gev
         if world > 1:
-            gev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        render_frame()
-        frame_end()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            if world > 1 and events:
+                gev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            render_frame()
+            frame_end(to_host)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        gev = None
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    dt = timed(False, True)
     # path_kernel alone: the library's HIP events around each launch on the launch stream, all K
     # steps (a render call splits a frame larger than 2^32 paths into several passes, one launch each)
     # every frame rendered so far is valid: no traversal guard tripped (raises otherwise)
@@ -402,6 +415,10 @@ def main() -> int:
                          "(ring of 64 overflowed or launches missing; lower --steps)")
     passes = len(pk) // (args.steps * launches)
     frame_kernel_ms = float(sum(pk)) / args.steps
+    # the same K steps with rank 0 copying the frame to pinned host memory in each (PCIe-inclusive; never `value`)
+    dt_host = dt if multi else timed(True, False)
+    for d in (range(multi) if multi else [dev]):
+        scene.path_kernel_times(d)
 
     value = frame_rays * args.steps / dt / 1e6
     # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +
@@ -497,6 +514,10 @@ def main() -> int:
                        "parallelism": f"tiles{n_dev}" + ("-single-process" if multi else "")},
             "roofline": roof,
             "paths_per_sec": round(w * h * spp * args.steps / dt, 1),
+            "pcie_inclusive": {"value": round(frame_rays * args.steps / dt_host / 1e6, 2),
+                               "ms_per_step": round(dt_host / args.steps * 1e3, 3),
+                               "note": "the same K steps with rank 0 copying the frame (w x h x 3 f32) to pinned host "
+                                       "memory in each: the rate through rtw_render's host-buffer boundary"},
         }
         if multi_gpu:
             out["multi_gpu"] = multi_gpu

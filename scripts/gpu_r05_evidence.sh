@@ -25,6 +25,11 @@ if [ -z "$NOTEST" ]; then
   fi
   grep -c '"n_gpus"' gpurun_out/${TAG}gpus2_no_launcher.log && { echo "a bench line was printed"; exit 1; }
   tail -1 gpurun_out/${TAG}gpus2_no_launcher.log
+  # the N > 1 bench path rehearsed on this one GPU: 2 ranks, gloo gather, the gathered frame checked bit for bit
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29511 bench.py --gpus 2 --steps 1 --warmup 1 --spp 32 --backend gloo --check-image \
+    > gpurun_out/${TAG}multirank_gloo2.log 2>&1 || { tail -5 gpurun_out/${TAG}multirank_gloo2.log; exit 1; }
+  grep -h "check_image" gpurun_out/${TAG}multirank_gloo2.log
 fi
 cd /tmp && export TMPDIR=/tmp
 for c in ${CONFIGS:-jumpy-1080p cornell-800 cow-1080p monument-4k}; do
