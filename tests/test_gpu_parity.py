@@ -89,6 +89,29 @@ def test_tiles_match_full_frame(gpu):
         assert np.array_equal(img.cpu().numpy().view(np.uint32), full.view(np.uint32)), world
 
 
+@pytest.mark.parametrize("scene,w,h,spp", [(None, 16, 8, 3), ("jumpy-balls", 2, 2, 1), ("cornell-box", 9, 3, 1),
+                                            ("wavefront-cow-obj", 2, 2, 5)])
+def test_empty_world_and_smallest_frames(gpu, orc, scene, w, h, spp):
+    """Edge cases of lib.rs:57-117: a world with no objects (every ray misses: the background, one ray per path,
+    the F_LIST kernel with an empty list), the smallest frame the reference can divide by (2 x 2: w - 1 = h - 1 = 1),
+    a single-row-of-tiles ragged frame, and one sample per pixel (the path id decode without the spp division).
+    These frames also take the small-frame batches."""
+    rtw = gpu
+    s = rtw.Scene()
+    if scene is None:
+        cam, bg = rtw.Camera.new((0, 0, 5), (0, 0, 0), (0, 1, 0), 40.0, w / h, 0.1, 5.0), (0.7, 0.8, 1.0)
+    else:
+        cam, bg = s.preset(scene, w / h, seed=3)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    g, st = rtw.Raytracer(s, cam, bg, w, h, spp, seed=7).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, w, h, spp, seed=7)
+    assert st["rays"] == rays
+    if scene is None:
+        assert rays == w * h * spp
+    assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
 def test_error_paths(gpu):
     rtw = gpu
     s = rtw.Scene()
@@ -117,7 +140,8 @@ def test_stack_spill_bit_exact(gpu, orc, knobs, name, aspect, w, h, spp):
                                   "RTW_LEAF16=16", "RTW_LDS_NODES=0", "RTW_OCC=5", "RTW_HALF_NODES=1",
                                   "RTW_HALF_NODES=0", "RTW_TRI_LEAF=0", "RTW_LDSN_WAVES=6", "RTW_LDSN_WAVES=7",
                                   "RTW_LDSN_BLK=512", "RTW_MESH_S16=0", "RTW_MESH_S16=6",
-                                  "RTW_MESH_S16=7", "RTW_BVH_PAIR=1", "RTW_BVH_BINS=64"])
+                                  "RTW_MESH_S16=7", "RTW_BVH_PAIR=1", "RTW_BVH_BINS=64", "RTW_BATCH=64",
+                                  "RTW_BATCH=65536"])
 def test_scheduling_knobs_bit_exact(gpu, orc, knobs, knob):
     """When a wave regenerates paths (RenderArgs::regen_min) and when a suspended traversal
     yields (quota16) change only which lanes run which path when; every path's draws and
