@@ -90,11 +90,12 @@ def test_tiles_match_full_frame(gpu):
 
 
 @pytest.mark.parametrize("scene,w,h,spp", [(None, 16, 8, 3), ("jumpy-balls", 2, 2, 1), ("cornell-box", 9, 3, 1),
-                                            ("wavefront-cow-obj", 2, 2, 5)])
+                                            ("wavefront-cow-obj", 2, 2, 5), ("jumpy-balls", 65536, 2, 1)])
 def test_empty_world_and_smallest_frames(gpu, orc, scene, w, h, spp):
     """Edge cases of lib.rs:57-117: a world with no objects (every ray misses: the background, one ray per path,
     the F_LIST kernel with an empty list), the smallest frame the reference can divide by (2 x 2: w - 1 = h - 1 = 1),
-    a single-row-of-tiles ragged frame, and one sample per pixel (the path id decode without the spp division).
+    a single-row-of-tiles ragged frame, the widest frame the 16-bit pixel coordinates of the path key allow
+    (65536 columns), and one sample per pixel (the path id decode without the spp division).
     These frames also take the small-frame batches."""
     rtw = gpu
     s = rtw.Scene()
@@ -121,6 +122,8 @@ def test_error_paths(gpu):
     cam = rtw.Camera.new((0, 0, 5), (0, 0, 0), (0, 1, 0), 40, 1.0, 0.0, 1.0)
     with pytest.raises(rtw.RtwError):
         rtw.Raytracer(s, cam, (0, 0, 0), 1, 1, 1).render()  # lib.rs:84-85 divides by w-1
+    with pytest.raises(rtw.RtwError):
+        rtw.Raytracer(s, cam, (0, 0, 0), 65537, 2, 1).render()  # beyond the path key's 16-bit column
     with pytest.raises(rtw.RtwError):
         s.sphere((0, 0, 0), 1, m)  # scene immutable after commit
 
