@@ -1,0 +1,132 @@
+"""Exact-t ties: the later object wins (hittable/mod.rs:61-65 tests every object against the closest t so far, and
+the primitives reject only t > t_max: spherical.rs:40-43, rectangular.rs:40, triangular.rs:118).
+
+Worlds of coincident primitives with different materials make every hit on them an exact tie, so the colour of the
+image depends on the tie rule alone.  Each kernel family must pick the later object in the hierarchy's depth-first
+order -- the sphere worlds' LDS-node BVH4 walk with its 32-B branch-free test, the rect list loop (`t <= best`), the
+rect BVH kernel, the triangle-leaf fast path (key read only on a candidate at or below the best t), instanced
+cuboids -- bit for bit against the oracle's flat list.  Each world is also rendered with the two copies swapped:
+the image must change, or the ties decided nothing."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W, H, SPP = 48, 27, 2
+
+
+def _render(rtw, orc, build, cam, bg):
+    s = rtw.Scene()
+    build(s, False)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    g, st = rtw.Raytracer(s, cam, bg, W, H, SPP, seed=13).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, SPP, seed=13)
+    assert st["rays"] == rays
+    bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
+    s2 = rtw.Scene()
+    build(s2, True)
+    s2.commit()
+    g2, _ = rtw.Raytracer(s2, cam, bg, W, H, SPP, seed=13).render()
+    assert not np.array_equal(g, g2), "swapping the coincident copies left the image unchanged: no tie was decided"
+    return s
+
+
+def _mats(s):
+    return s.lambertian_solid((0.9, 0.15, 0.1)), s.lambertian_solid((0.1, 0.8, 0.2))
+
+
+def test_coincident_spheres_lds_node_walk(gpu, orc):
+    """80 spheres added twice (static, then as moving spheres that do not move) over a ground sphere: a BVH'd
+    sphere world, so the LDS-node kernel's walk and its 32-B test decide the ties."""
+    rtw = gpu
+    rng = np.random.default_rng(5)
+    c = np.stack([rng.uniform(-6, 6, 80), rng.uniform(0.2, 1.5, 80), rng.uniform(-6, 6, 80)], 1).astype(np.float32)
+    r = rng.uniform(0.2, 0.6, 80).astype(np.float32)
+
+    def build(s, swap):
+        a, b = _mats(s)
+        first, second = (b, a) if swap else (a, b)
+        ground = s.lambertian_solid((0.5, 0.5, 0.5))
+        s.sphere((0, -1000, 0), 1000, ground)
+        s.spheres(c, r, [first] * len(r))
+        s.moving_spheres(c, np.zeros(len(r)), c, np.ones(len(r)), r, [second] * len(r))
+
+    cam = rtw.Camera.new((13, 2, 3), (0, 0, 0), (0, 1, 0), 30.0, W / H, 0.0, 10.0)
+    s = _render(rtw, orc, build, cam, (0.7, 0.8, 1.0))
+    assert s.info(3) > 0  # a BVH, not the list
+
+
+def test_coincident_rects_list_loop_and_instances(gpu, orc):
+    """A box of walls, each wall twice, and two rotated + translated cuboids, each twice: a list-mode world of 24
+    rects (the rect list loop and its per-chain reciprocals)."""
+    rtw = gpu
+
+    def build(s, swap):
+        a, b = _mats(s)
+        first, second = (b, a) if swap else (a, b)
+        light = s.diffuse_light(s.solid_rgb(8, 8, 8))
+        for m in (first, second):
+            s.yz_rect(0, 555, 0, 555, 555, m)
+            s.yz_rect(0, 555, 0, 555, 0, m)
+            s.xz_rect(0, 555, 0, 555, 0, m)
+            s.xy_rect(0, 555, 0, 555, 555, m)
+        s.xz_rect(113, 443, 127, 432, 554, light)
+        for m in (first, second):
+            with s.translate((265, 0, 295)):
+                with s.rotate_y(15):
+                    s.cuboid((0, 0, 0), (165, 330, 165), m)
+        s.xz_rect(0, 555, 0, 555, 555, first)
+
+    cam = rtw.Camera.new((278, 278, -800), (278, 278, 0), (0, 1, 0), 40.0, W / H, 0.0, 10.0)
+    s = _render(rtw, orc, build, cam, (0.0, 0.0, 0.0))
+    assert s.info(3) == 0  # list mode
+
+
+def test_coincident_rects_bvh(gpu, orc):
+    """40 small rects, each twice (80 > the 32-prim list limit): the rect BVH kernel's leaves decide the ties."""
+    rtw = gpu
+    rng = np.random.default_rng(9)
+    x0 = rng.uniform(-5, 4, 40).astype(np.float32)
+    y0 = rng.uniform(-3, 2, 40).astype(np.float32)
+    k = rng.uniform(-4, 0, 40).astype(np.float32)
+
+    def build(s, swap):
+        a, b = _mats(s)
+        first, second = (b, a) if swap else (a, b)
+        for m in (first, second):
+            s.rects([0] * 40, x0, x0 + 1.5, y0, y0 + 1.5, k, [m] * 40)
+
+    cam = rtw.Camera.new((0, 0, 8), (0, 0, 0), (0, 1, 0), 60.0, W / H, 0.0, 8.0)
+    s = _render(rtw, orc, build, cam, (0.7, 0.8, 1.0))
+    assert s.info(3) > 0
+
+
+def test_coincident_triangles_mesh_leaves(gpu, orc):
+    """A 12 x 12 grid of 288 triangles, added twice: every BVH leaf is a triangle of one chain, so the triangle
+    leaf fast path decides the ties (its key load only for candidates at or below the best t)."""
+    rtw = gpu
+    n = 12
+    g = np.linspace(-4, 4, n + 1, dtype=np.float32)
+    tris = []
+    for i in range(n):
+        for j in range(n):
+            p00 = (g[i], g[j], -0.3 * g[i])
+            p10 = (g[i + 1], g[j], -0.3 * g[i + 1])
+            p01 = (g[i], g[j + 1], -0.3 * g[i])
+            p11 = (g[i + 1], g[j + 1], -0.3 * g[i + 1])
+            tris += [p00, p10, p11, p00, p11, p01]
+    verts = np.asarray(tris, np.float32).reshape(-1)
+
+    def build(s, swap):
+        a, b = _mats(s)
+        first, second = (b, a) if swap else (a, b)
+        with s.translate((0.0, 0.5, 0.0)):
+            s.triangles(verts, first)
+            s.triangles(verts, second)
+        s.xz_rect(-20, 20, -20, 20, 30, s.diffuse_light(s.solid_rgb(2, 2, 2)))
+
+    cam = rtw.Camera.new((2, 1, 9), (0, 0, 0), (0, 1, 0), 50.0, W / H, 0.0, 9.0)
+    s = _render(rtw, orc, build, cam, (0.3, 0.3, 0.35))
+    assert s.info(3) > 0
