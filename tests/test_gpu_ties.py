@@ -130,3 +130,42 @@ def test_coincident_triangles_mesh_leaves(gpu, orc):
     cam = rtw.Camera.new((2, 1, 9), (0, 0, 0), (0, 1, 0), 50.0, W / H, 0.0, 9.0)
     s = _render(rtw, orc, build, cam, (0.3, 0.3, 0.35))
     assert s.info(3) > 0
+
+
+def test_degenerate_primitives(gpu, orc):
+    """Degenerate inputs the reference accepts without complaint render as the oracle does: zero-area triangles (a
+    repeated vertex, collinear vertices: det = 0, t = NaN fails `t >= 0`), slivers (|det| tiny, 1 / det huge), a
+    zero-radius sphere, a hollow (negative-radius) glass sphere, zero-width and inverted-bounds rects (never hit:
+    rectangular.rs:40 cannot pass with a0 > a1), next to ordinary geometry."""
+    rtw = gpu
+    rng = np.random.default_rng(21)
+    tris = []
+    for _ in range(40):  # ordinary triangles
+        p = rng.uniform(-3, 3, 3).astype(np.float32)
+        tris += [p, p + rng.uniform(-1, 1, 3), p + rng.uniform(-1, 1, 3)]
+    for _ in range(20):  # repeated vertex / collinear / sliver
+        p = rng.uniform(-3, 3, 3).astype(np.float32)
+        q = p + rng.uniform(-1, 1, 3).astype(np.float32)
+        tris += [p, p, q]
+        tris += [p, q, p + np.float32(2.0) * (q - p)]
+        tris += [p, q, q + np.float32(1e-6) * rng.uniform(-1, 1, 3).astype(np.float32)]
+    verts = np.asarray(tris, np.float32).reshape(-1)
+    s = rtw.Scene()
+    a, b = _mats(s)
+    glass = s.dielectric(1.5)
+    s.triangles(verts, a)
+    s.sphere((0, 0, 0), 0.0, b)
+    s.sphere((1, 0.5, 1), 0.8, glass)
+    s.sphere((1, 0.5, 1), -0.7, glass)
+    s.xy_rect(-2, -2, -2, 2, -3, b)   # zero width
+    s.xz_rect(2, -2, -2, 2, -2.5, b)  # inverted bounds
+    s.xz_rect(-50, 50, -50, 50, -4, s.lambertian_solid((0.5, 0.5, 0.5)))
+    cam = rtw.Camera.new((3, 2, 8), (0, 0, 0), (0, 1, 0), 50.0, W / H, 0.0, 8.0)
+    bg = (0.7, 0.8, 1.0)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    g, st = rtw.Raytracer(s, cam, bg, W, H, 4, seed=3).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, 4, seed=3)
+    assert st["rays"] == rays
+    bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
