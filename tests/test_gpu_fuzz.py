@@ -97,3 +97,34 @@ def test_random_world_bit_exact(gpu, orc, seed):
     bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}: " \
                           f"gpu {g[tuple(bad[0][:2])]} oracle {r[tuple(bad[0][:2])]}"
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_mesh_bit_exact(gpu, orc, seed):
+    """Random triangle soups of 1,500-6,000 triangles under one Translation, with a light rect and a checkered ground
+    sphere: the mesh kernels (F_MESHES: triangle-only BVH leaves, half-precision nodes where built, the 16-bit-stack
+    walk) on trees nobody tuned."""
+    rtw = gpu
+    rng = np.random.default_rng(2000 + seed)
+    n = int(rng.integers(1500, 6000))
+    s = rtw.Scene()
+    white = s.lambertian_solid((0.73, 0.73, 0.73))
+    img = s.lambertian(s.image(rng.integers(0, 256, (16, 16, 3), dtype=np.uint8)))
+    light = s.diffuse_light(s.solid_rgb(4, 4, 4))
+    ground = s.lambertian(s.checker(s.solid_rgb(0.2, 0.3, 0.1), s.solid_rgb(0.9, 0.9, 0.9), 10.0))
+    p = rng.normal(0, 1.5, (n, 1, 3)).astype(np.float32) + rng.uniform(-0.3, 0.3, (n, 3, 3)).astype(np.float32)
+    uv = rng.uniform(0, 1, (n, 3, 2)).astype(np.float32)
+    with s.translate(tuple(rng.uniform(-1, 1, 3))):
+        s.triangles(p.reshape(-1), img if seed % 2 else white, uvs=uv.reshape(-1) if seed % 2 else None)
+    s.xz_rect(-3, 3, -3, 3, 6, light)
+    s.sphere((0, -1000, 0), 995, ground)
+    cam = rtw.Camera.new((float(rng.uniform(-8, 8)), 2.0, 9.0), (0, 0, 0), (0, 1, 0), 45.0, W / H, 0.0, 9.0)
+    bg = (0.1, 0.1, 0.15)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    g, st = rtw.Raytracer(s, cam, bg, W, H, SPP, seed=seed).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, SPP, seed=seed)
+    assert st["rays"] == rays
+    bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
+    assert s.info(3) > 0
