@@ -52,6 +52,9 @@ def lib() -> C.CDLL:
             "oracle_render": (C.c_int, [C.c_void_p, C.POINTER(oracle_camera), _F, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_int, _U32,
                                         C.c_uint32, _F, C.POINTER(C.c_uint64)]),
+            "oracle_render_counts": (C.c_int, [C.c_void_p, C.POINTER(oracle_camera), _F, C.c_uint32, C.c_uint32,
+                                               C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_int, _U32,
+                                               C.c_uint32, _F, C.POINTER(C.c_uint64), _U32]),
             "oracle_pcg32_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
             "oracle_rng_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
             "oracle_splitmix64": (C.c_uint64, [C.c_uint64]),
@@ -124,18 +127,21 @@ class OracleScene:
         return lib().oracle_scene_count(self._p, what)
 
     def render(self, cam: oracle_camera, background, w, h, spp, seed=0, max_depth=50,
-               integrator=ITERATIVE, bvh_mode=BVH_AS_LIST, threads=None, rows=None):
-        """-> (sums[h, w, 3] in reference order, rays).  rows: list of j (bottom-based) to render."""
+               integrator=ITERATIVE, bvh_mode=BVH_AS_LIST, threads=None, rows=None, pixel_rays=False):
+        """-> (sums[h, w, 3] in reference order, rays[, per-pixel rays[h, w] when pixel_rays]).
+        rows: list of j (bottom-based) to render."""
         out = np.zeros((h, w, 3), np.float32)
         rays = C.c_uint64()
+        pr = np.zeros((h, w), np.uint32) if pixel_rays else None
         r = np.ascontiguousarray(rows, np.uint32) if rows is not None else None
         n = threads or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
-        rc = lib().oracle_render(self._p, C.byref(cam), fp(f32(background)), w, h, spp, max_depth, seed,
-                                 integrator, bvh_mode, n, r.ctypes.data_as(_U32) if r is not None else None,
-                                 len(r) if r is not None else 0, fp(out), C.byref(rays))
+        rc = lib().oracle_render_counts(self._p, C.byref(cam), fp(f32(background)), w, h, spp, max_depth, seed,
+                                        integrator, bvh_mode, n, r.ctypes.data_as(_U32) if r is not None else None,
+                                        len(r) if r is not None else 0, fp(out), C.byref(rays),
+                                        pr.ctypes.data_as(_U32) if pr is not None else None)
         if rc != 0:
             raise RuntimeError(lib().oracle_last_error().decode())
-        return out, int(rays.value)
+        return (out, int(rays.value), pr) if pixel_rays else (out, int(rays.value))
 
 
 def libm(fn: int, a, b=None) -> np.ndarray:

@@ -902,11 +902,23 @@ static vec3 sample_ray_rec(ctx_t* c, const ray* r, draws* d, uint32_t depth) {
 /* The same estimator, evaluated front-to-back as the GPU does: L = T * terminal with
  * T = ((a0*a1)*a2)...  Identical paths and draws; the product differs from the literal
  * right-to-left recursion only by rounding (tolerance stated in tests). */
+/* Debug aid (test infrastructure): ORACLE_TRACE="j,i,s" prints that path's segments to stderr. */
+static __thread int g_trace;
 static vec3 sample_ray_iter(ctx_t* c, ray r, draws* d, uint32_t depth) {
   vec3 T = v3(1.0f, 1.0f, 1.0f);
   for (; depth > 0; --depth) {
     hitrec h;
-    if (!world_hit(c, &r, d, &h)) return vmul(T, c->bg);
+    const int hit = world_hit(c, &r, d, &h);
+    if (g_trace) {
+      fprintf(stderr, "depth %u o (%a %a %a) d (%a %a %a) time %a rng %016llx", depth, r.o.x, r.o.y, r.o.z, r.d.x,
+              r.d.y, r.d.z, r.time, (unsigned long long)d->rng.s);
+      if (hit)
+        fprintf(stderr, " -> t %a p (%a %a %a) n (%a %a %a) mat %d front %d\n", h.t, h.p.x, h.p.y, h.p.z, h.n.x,
+                h.n.y, h.n.z, h.mat, h.front);
+      else
+        fprintf(stderr, " -> miss\n");
+    }
+    if (!hit) return vmul(T, c->bg);
     const omat* m = &c->s->mat[h.mat];
     scatter_t sc;
     if (!mat_scatter(c->s, m, &r, &h, d, &sc)) return vmul(T, mat_emitted(c->s, m, &h));
@@ -926,6 +938,7 @@ typedef struct {
   const uint32_t* rows;
   uint32_t n_rows;
   float* out;
+  uint32_t* pixel_rays;
   atomic_uint next;
   atomic_ullong rays;
 } job_t;
@@ -933,6 +946,9 @@ typedef struct {
 static void* worker(void* arg) {
   job_t* jb = (job_t*)arg;
   ctx_t c = {jb->s, jb->bg, jb->bvh_mode, 0};
+  long tj = -1, ti = -1, ts = -1;
+  const char* tr = getenv("ORACLE_TRACE");
+  if (tr) sscanf(tr, "%ld,%ld,%ld", &tj, &ti, &ts);
   for (;;) {
     uint32_t k = atomic_fetch_add(&jb->next, 1u);
     if (k >= jb->n_rows) break;
@@ -940,10 +956,12 @@ static void* worker(void* arg) {
     for (uint32_t i = 0; i < jb->w; ++i) {
       /* lib.rs:78-95 */
       vec3 sum = v3(0, 0, 0);
+      const uint64_t rays0 = c.rays;
       for (uint32_t sidx = 0; sidx < jb->spp; ++sidx) {
         draws d;
         memset(&d, 0, sizeof d);
         d.rng.s = oracle_path_state(jb->seed, j, i, sidx);
+        g_trace = (long)j == tj && (long)i == ti && (long)sidx == ts;
         float u = ((float)i + gen_f32(&d)) / (float)(jb->w - 1u);
         float v = ((float)j + gen_f32(&d)) / (float)(jb->h - 1u);
         ray r = camera_get_ray(jb->cam, u, v, &d);
@@ -953,6 +971,7 @@ static void* worker(void* arg) {
       }
       float* o = jb->out + ((size_t)(jb->h - 1u - j) * jb->w + i) * 3;
       o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
+      if (jb->pixel_rays) jb->pixel_rays[(size_t)(jb->h - 1u - j) * jb->w + i] = (uint32_t)(c.rays - rays0);
     }
   }
   atomic_fetch_add(&jb->rays, c.rays);
@@ -963,6 +982,13 @@ int oracle_render(oracle_scene* s, const oracle_camera* cam, const float backgro
                   uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, int integrator,
                   int bvh_mode, int n_threads, const uint32_t* rows, uint32_t n_rows, float* out,
                   uint64_t* rays) {
+  return oracle_render_counts(s, cam, background, w, h, spp, max_depth, seed, integrator, bvh_mode, n_threads, rows,
+                              n_rows, out, rays, NULL);
+}
+int oracle_render_counts(oracle_scene* s, const oracle_camera* cam, const float background[3], uint32_t w,
+                         uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, int integrator,
+                         int bvh_mode, int n_threads, const uint32_t* rows, uint32_t n_rows, float* out,
+                         uint64_t* rays, uint32_t* pixel_rays) {
   if (!s || !cam || !out || w < 2 || h < 2) { set_err("bad arguments"); return -22; }
   if (w > 65536 || h > 65536) { set_err("w, h <= 65536 (16-bit pixel coordinates in the path key)"); return -22; }
   job_t jb;
@@ -972,6 +998,7 @@ int oracle_render(oracle_scene* s, const oracle_camera* cam, const float backgro
   jb.integrator = integrator; jb.bvh_mode = bvh_mode;
   jb.rows = rows; jb.n_rows = rows ? n_rows : h;
   jb.out = out;
+  jb.pixel_rays = pixel_rays;
   atomic_init(&jb.next, 0u);
   atomic_init(&jb.rays, 0ull);
   if (n_threads < 1) n_threads = 1;

@@ -56,6 +56,12 @@ int oracle_render(oracle_scene* s, const oracle_camera* cam, const float backgro
                   uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
                   int integrator, int bvh_mode, int n_threads,
                   const uint32_t* rows, uint32_t n_rows, float* out, uint64_t* rays);
+/* The same, also writing each pixel's ray count (all spp samples) into pixel_rays[(H-1-j)*W + i] when non-NULL
+ * (a debugging aid: locates paths whose segment counts differ from the GPU's). */
+int oracle_render_counts(oracle_scene* s, const oracle_camera* cam, const float background[3],
+                         uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
+                         int integrator, int bvh_mode, int n_threads,
+                         const uint32_t* rows, uint32_t n_rows, float* out, uint64_t* rays, uint32_t* pixel_rays);
 
 /* ---- unit-level entry points used by the KAT / golden-vector tests ---- */
 uint32_t oracle_pcg32_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t* state_out);

@@ -1665,6 +1665,12 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     ts.on = false;
     if (COUNT) simd_tick(cnt, 12, 13);
     const Best b = ts.b;
+#ifdef RTW_DIAG_TRACE_PID  // debugging aid (never in the product build): one path's segments via device printf
+    if ((RTW_DIAG_TRACE_PID) < 0 || st.pid == (uint32_t)(RTW_DIAG_TRACE_PID))  // < 0: every path
+      printf("rtwtrace pid %u o %a %a %a d %a %a %a t %a prim %d key %u rng %016llx\n", st.pid, st.ray.o.x, st.ray.o.y,
+             st.ray.o.z, st.ray.d.x, st.ray.d.y, st.ray.d.z, b.t, b.prim, b.prim >= 0 ? S.prims[b.prim].key : 0u,
+             (unsigned long long)st.rng);
+#endif
     bool done = false;
     V3 L = mk(0.f, 0.f, 0.f);
     // the throughput; the S16 mesh walk reads it from its LDS rows where it is used, after the hit record and the

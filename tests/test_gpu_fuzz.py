@@ -14,7 +14,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-W, H, SPP = 40, 24, 2
+W, H, SPP = (int(x) for x in os.environ.get("RTW_FUZZ_FRAME", "40,24,2").split(","))
 
 
 def _build(rtw, s, rng):
@@ -99,7 +99,7 @@ def test_random_world_bit_exact(gpu, orc, seed):
                           f"gpu {g[tuple(bad[0][:2])]} oracle {r[tuple(bad[0][:2])]}"
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("RTW_FUZZ_MESH_SEEDS", "6"))))
 def test_random_mesh_bit_exact(gpu, orc, seed):
     """Random triangle soups of 1,500-6,000 triangles under one Translation, with a light rect and a checkered ground
     sphere: the mesh kernels (F_MESHES: triangle-only BVH leaves, half-precision nodes where built, the 16-bit-stack
