@@ -718,7 +718,8 @@ struct TraceState {
 // TMIN <= best always, a0 <= a1 for every rect, DevScene::rect_fast): 3 med3 + 3 compares and 2 scalar ands instead
 // of 6 compares and 5.  A chain where any lane of the wave is outside that range runs the reference's IEEE
 // division and compares (slow path).  The list is in DFS-key order, so a later rect wins a tie: accept t <= best
-// (no key compare; bt starts at FLT_MAX, which also rejects t = inf).  VERDICT r4 item 3.
+// (no key compare; bt starts at the reference's t_max = inf: a fast-path t is finite).  VERDICT r4 item 3.
+constexpr int32_t RECT_NAN_HIT = 0x40000000;  // trace_rect_list's bp: the winner's t is NaN (list worlds: few prims)
 template <int AXIS, bool FAST>
 __device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, float4 q0, float k, uint32_t pi, float& bt,
                                                int32_t& bp) {
@@ -736,15 +737,22 @@ __device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, float4 q0, f
     acc = (__builtin_amdgcn_fmed3f(t, TMIN, bt) == t) & (__builtin_amdgcn_fmed3f(x, q0.x, q0.y) == x) &
           (__builtin_amdgcn_fmed3f(yy, q0.z, q0.w) == yy);
     bt = acc ? t : bt;
+    bp = acc ? (int32_t)pi : bp;
   } else {
+    // the reference's own comparisons, rejections that a NaN passes (rectangular.rs:33-41): a ray in the
+    // rect's plane (d_k = 0, k - o_k = 0: a Lambertian bounce whose direction lost its normal component) has
+    // t = 0 / 0 and hits.  The reference's best is then NaN, under which every later rect whose own test passes
+    // wins -- exactly as under best = +inf -- so bt keeps +inf (never NaN: the fast path's med3 needs an ordered
+    // bound) and bp carries RECT_NAN_HIT; trace_rect_list hands the winner on with t = NaN.
     const float t = num / d_k;
     const float x = o_a + t * d_a;
     const float yy = o_b + t * d_b;
     const bool out = (x < q0.x) | (x > q0.y) | (yy < q0.z) | (yy > q0.w);
-    acc = (t >= TMIN) & (t <= bt) & !out;
-    bt = acc ? t : bt;
+    acc = !(t < TMIN) & !(t > bt) & !out;
+    const bool tnan = t != t;
+    bt = acc ? (tnan ? INFINITY : t) : bt;
+    bp = acc ? ((int32_t)pi | (tnan ? RECT_NAN_HIT : 0)) : bp;
   }
-  bp = acc ? (int32_t)pi : bp;
 }
 
 // one run of rects of one kind (AXIS) and chain: the whole 64-B record in one scalar load (s_load_dwordx16)
@@ -770,7 +778,7 @@ __device__ __forceinline__ void rect_list_run(const DevScene& S, uint32_t first,
 
 template <bool COUNT>
 __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r, Best& best, uint32_t* cnt) {
-  float bt = 0x1.fffffep127f;  // FLT_MAX
+  float bt = INFINITY;  // lib.rs:102 t_max
   int32_t bp = -1;
   uint32_t cur = 0xFFFFFFFFu;
   Ray lr = r;
@@ -796,8 +804,10 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
       else rect_list_run<COUNT, 2, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
     }
   }
-  best.t = bt;
-  best.prim = bp;
+  // an in-plane hit won (RECT_NAN_HIT; bp < 0 = no hit): the reference's t is NaN
+  const bool nan_hit = bp >= 0 && (bp & RECT_NAN_HIT) != 0;
+  best.t = nan_hit ? __builtin_nanf("") : bt;
+  best.prim = nan_hit ? (bp & ~RECT_NAN_HIT) : bp;
 }
 
 template <bool COUNT, uint32_t FEAT>

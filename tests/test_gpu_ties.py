@@ -169,3 +169,36 @@ def test_degenerate_primitives(gpu, orc):
     assert st["rays"] == rays
     bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
+
+
+@pytest.mark.parametrize("tile,spp", [(2149, 20), (2347, 16)])
+def test_in_plane_bounce_list_mode(gpu, orc, tile, spp):
+    """A Lambertian bounce off cornell's floor whose direction lost its normal component exactly (d.y = 0, the
+    origin on the plane y = 0) meets the floor at t = 0 / 0 = NaN, and the reference's rejections (rectangular.rs:
+    33-41: `t < t_min || t > t_max`, then the bounds) all let a NaN through: it is a hit, best becomes NaN, every later
+    rect whose own test passes wins, and the path continues from a NaN origin to the depth limit.  The rect list
+    loop reproduces this on its IEEE path.  These two tiles of the 800 x 800 bench frame (scene seed 42, render seed
+    2024) hold the only two such events of its first 32 samples (scripts/count_bisect.py): their last sample is the
+    one with the in-plane bounce.  Packed tile render against the oracle's rows, bit for bit, with ray counts."""
+    torch = pytest.importorskip("torch")
+    rtw = gpu
+    w = h = 800
+    s = rtw.Scene()
+    cam, bg = s.preset("cornell-box", 1.0, seed=42)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    rt = rtw.Raytracer(s, cam, bg, w, h, spp, seed=2024)
+    ids = torch.tensor([tile], dtype=torch.int32, device="cuda:0")
+    packed = torch.zeros((1, 64, 3), dtype=torch.float32, device="cuda:0")
+    st = rt.render_device(packed.data_ptr(), 0, ids.data_ptr(), 1, torch.cuda.current_stream().cuda_stream,
+                          want_stats=True)
+    torch.cuda.synchronize()
+    r, c = divmod(tile, (w + 7) // 8)
+    rows = [h - 1 - (r * 8 + k) for k in range(8)]  # j of the tile's rows (output row 0 = j = h - 1)
+    ref, _, pr = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, w, h, spp, seed=2024,
+                                                    rows=rows, pixel_rays=True)
+    assert int(st["rays"]) == int(pr[r * 8:(r + 1) * 8, c * 8:(c + 1) * 8].sum())
+    want = ref[r * 8:(r + 1) * 8, c * 8:(c + 1) * 8].reshape(64, 3)
+    got = packed.cpu().numpy()[0]
+    bad = np.argwhere(got.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
