@@ -387,7 +387,7 @@ __device__ __forceinline__ float cand_sphere(const Ray& r, V3 c, float rad2) {  
   float hb = dot(oc, r.d);
   float cc = len2(oc) - rad2;
   float disc = hb * hb - a * cc;
-  if (!(disc >= 0.0f)) return -1.0f;
+  if (disc < 0.0f) return -1.0f;  // spherical.rs:32: a NaN discriminant goes on (a NaN root, a hit in list mode)
   float sq = sqrtf(disc);
   float root = (-hb - sq) / a;
   if (root < TMIN) root = (-hb + sq) / a;  // root1 > t_max implies root2 > t_max
@@ -585,6 +585,10 @@ __device__ __forceinline__ void test_sphere32(const DevScene& S, uint32_t pi, fl
   }
 }
 
+// List-mode kernels (F_LIST): a winner whose t is NaN (an in-plane hit, see rect_list_test) is carried with best
+// t = +inf and this bit in its index (list worlds have few prims); trace_begin hands it on with t = NaN
+constexpr int32_t RECT_NAN_HIT = 0x40000000;
+
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
 template <bool COUNT, uint32_t FEAT, bool LOCAL = false, bool UNI = false>
@@ -641,6 +645,21 @@ __device__ __forceinline__ void test_prim(const DevScene& S, uint32_t pi, const 
     else if (type == PT_RECT_YZ) t = cand_rect<2, SEL>(lr, q0, k);
   }
   if (COUNT) { cnt[1]++; if (type < 6u) cnt[2 + type]++; simd_tick(cnt, 10, 11); }  // media: total only
+  if constexpr ((FEAT & F_LIST) != 0) {
+    // list mode tests in DFS-key order: the reference's own fold (hittable/mod.rs:57-69) with its comparisons,
+    // which a NaN candidate passes (rectangular.rs:33-41, spherical.rs:32-43): best NaN behaves as best +inf
+    // (RECT_NAN_HIT); a later object wins ties by order
+    const bool acc = !(t < TMIN) & !(t > b.t);
+    const bool tnan = t != t;
+    b.t = acc ? (tnan ? INFINITY : t) : b.t;
+    b.key = acc ? meta.y : b.key;
+    b.prim = acc ? ((int32_t)pi | (tnan ? RECT_NAN_HIT : 0)) : b.prim;
+    if (FEAT & F_TRI) {
+      b.u = acc ? tu : b.u;
+      b.v = acc ? tv : b.v;
+    }
+    return;
+  }
   // hittable/mod.rs:61-65: accept t <= closest_so_far; a later object (larger key) wins ties
   if constexpr (SEL) {
     const bool acc = (t >= TMIN) & (t < INFINITY) & ((t < b.t) | ((t == b.t) & (meta.y > b.key)));
@@ -719,7 +738,6 @@ struct TraceState {
 // of 6 compares and 5.  A chain where any lane of the wave is outside that range runs the reference's IEEE
 // division and compares (slow path).  The list is in DFS-key order, so a later rect wins a tie: accept t <= best
 // (no key compare; bt starts at the reference's t_max = inf: a fast-path t is finite).  VERDICT r4 item 3.
-constexpr int32_t RECT_NAN_HIT = 0x40000000;  // trace_rect_list's bp: the winner's t is NaN (list worlds: few prims)
 template <int AXIS, bool FAST>
 __device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, float4 q0, float k, uint32_t pi, float& bt,
                                                int32_t& bp) {
@@ -843,6 +861,11 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     // (the loaded index here: the computed one made the sphere kernels 1.1% slower, experiments a1)
     for (uint32_t k = 0; k < S.n_always; ++k)
       test_prim<COUNT, FEAT, false, true>(S, uload(S.always + k), r, ts.b, cnt, seg, SPH_ONLY ? &rq : nullptr);
+  }
+  if constexpr ((FEAT & F_LIST) && !RECT_LIST) {  // an in-plane (NaN) winner: the reference's t is NaN
+    const bool nan_hit = ts.b.prim >= 0 && (ts.b.prim & RECT_NAN_HIT) != 0;
+    ts.b.t = nan_hit ? __builtin_nanf("") : ts.b.t;
+    ts.b.prim = nan_hit ? (ts.b.prim & ~RECT_NAN_HIT) : ts.b.prim;
   }
   // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR across the
   // whole loop and spilled it.  Triangle kernels (the mesh walk): as a scalar, since the 7-wave walk spilled even
@@ -2152,7 +2175,7 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
     // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
     // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
     // at 8; knob RTW_LIST_OCC); the all-features one spills below 96 VGPRs, so it stays at 5.
-    if ((feat & ~F_BOXES) == 0) {
+    if ((feat & ~F_BOXES) == 0 && !env_int("RTW_LIST_ALL", 0)) {  // knob: the all-features list kernel instead
       if (env_int("RTW_LIST_OCC", 8) == 6) return {path_kernel<C, 1, false, 6, F_BOXES | F_LIST>, 1u};
       return {path_kernel<C, 1, false, 8, F_BOXES | F_LIST>, 1u};
     }

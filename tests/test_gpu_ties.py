@@ -171,17 +171,21 @@ def test_degenerate_primitives(gpu, orc):
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
 
 
+@pytest.mark.parametrize("kernel", ["rect_list", "all_features_list"])
 @pytest.mark.parametrize("tile,spp", [(2149, 20), (2347, 16)])
-def test_in_plane_bounce_list_mode(gpu, orc, tile, spp):
+def test_in_plane_bounce_list_mode(gpu, orc, knobs, kernel, tile, spp):
     """A Lambertian bounce off cornell's floor whose direction lost its normal component exactly (d.y = 0, the
     origin on the plane y = 0) meets the floor at t = 0 / 0 = NaN, and the reference's rejections (rectangular.rs:
     33-41: `t < t_min || t > t_max`, then the bounds) all let a NaN through: it is a hit, best becomes NaN, every later
     rect whose own test passes wins, and the path continues from a NaN origin to the depth limit.  The rect list
     loop reproduces this on its IEEE path.  These two tiles of the 800 x 800 bench frame (scene seed 42, render seed
     2024) hold the only two such events of its first 32 samples (scripts/count_bisect.py): their last sample is the
-    one with the in-plane bounce.  Packed tile render against the oracle's rows, bit for bit, with ray counts."""
+    one with the in-plane bounce.  Packed tile render against the oracle's rows, bit for bit, with ray counts; through
+    the rect list loop and through the all-features list kernel (knob RTW_LIST_ALL: test_prim's list fold)."""
     torch = pytest.importorskip("torch")
     rtw = gpu
+    if kernel == "all_features_list":
+        knobs.setenv("RTW_LIST_ALL", "1")
     w = h = 800
     s = rtw.Scene()
     cam, bg = s.preset("cornell-box", 1.0, seed=42)
