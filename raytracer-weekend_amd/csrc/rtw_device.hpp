@@ -49,6 +49,8 @@ static_assert(sizeof(DevPrim) == 64, "DevPrim must be 64 B");
 struct alignas(16) DevGroup {
   uint32_t first, count, inst, type;
 };
+// DevGroup::type of a whole Cuboid (rectangular.rs:177-240: xy, xy, xz, xz, yz, yz, one chain) as one run
+constexpr uint32_t GK_BOX6 = 16u;
 static_assert(sizeof(DevGroup) == 16, "DevGroup must be 16 B");
 
 struct alignas(16) DevNode {

@@ -740,6 +740,23 @@ int flatten(Scene& s) {
     else
       f.lgroups.push_back(DevGroup{f.always[k], 1u, inst, type});
   }
+  {  // a Cuboid's three pair runs as one (GK_BOX6): one dispatch in the kernel's run loop instead of three
+    std::vector<DevGroup> g2;
+    for (size_t g = 0; g < f.lgroups.size(); ++g) {
+      const DevGroup& a = f.lgroups[g];
+      if (g + 2 < f.lgroups.size()) {
+        const DevGroup &b = f.lgroups[g + 1], &c = f.lgroups[g + 2];
+        if (a.type == PT_RECT_XY && b.type == PT_RECT_XZ && c.type == PT_RECT_YZ && a.count == 2u && b.count == 2u &&
+            c.count == 2u && a.inst == b.inst && b.inst == c.inst && b.first == a.first + 2u && c.first == b.first + 2u) {
+          g2.push_back(DevGroup{a.first, 6u, a.inst, GK_BOX6});
+          g += 2;
+          continue;
+        }
+      }
+      g2.push_back(a);
+    }
+    f.lgroups.swap(g2);
+  }
   // spheres carry their DFS key in q1[3] too (the sphere-only kernels' 32-B test, rtw_device.hpp)
   for (DevPrim& p : f.prims) {
     const uint32_t t = p.type_inst & 0xffu;

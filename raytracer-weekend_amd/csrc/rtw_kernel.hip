@@ -805,6 +805,15 @@ __device__ __forceinline__ void rect_list_run(const DevScene& S, uint32_t first,
   }
 }
 
+// a whole Cuboid (GK_BOX6): its xy, xz and yz pairs back to back, no run dispatch between them
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ void rect_box6_run(const DevScene& S, uint32_t first, const Ray& lr, V3 y, float& bt,
+                                              int32_t& bp, uint32_t* cnt) {
+  rect_list_run<COUNT, 0, FAST>(S, first, 2u, lr, y, bt, bp, cnt);
+  rect_list_run<COUNT, 1, FAST>(S, first + 2u, 2u, lr, y, bt, bp, cnt);
+  rect_list_run<COUNT, 2, FAST>(S, first + 4u, 2u, lr, y, bt, bp, cnt);
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r, Best& best, uint32_t* cnt) {
   float bt = INFINITY;  // lib.rs:102 t_max
@@ -824,11 +833,13 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
       fast = S.rect_fast && __ballot(!ok) == 0;
     }
     if (fast) {
-      if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      if (G.w == GK_BOX6) rect_box6_run<COUNT, true>(S, G.x, lr, y, bt, bp, cnt);
+      else if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
       else if (G.w == PT_RECT_XZ) rect_list_run<COUNT, 1, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
       else rect_list_run<COUNT, 2, true>(S, G.x, G.y, lr, y, bt, bp, cnt);
     } else {
-      if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
+      if (G.w == GK_BOX6) rect_box6_run<COUNT, false>(S, G.x, lr, y, bt, bp, cnt);
+      else if (G.w == PT_RECT_XY) rect_list_run<COUNT, 0, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
       else if (G.w == PT_RECT_XZ) rect_list_run<COUNT, 1, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
       else rect_list_run<COUNT, 2, false>(S, G.x, G.y, lr, y, bt, bp, cnt);
     }
