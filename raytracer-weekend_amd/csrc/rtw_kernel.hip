@@ -828,8 +828,14 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
       cur = G.z;
       lr = cur ? to_local<true>(S.insts + cur, r) : r;
       y = mk(rcp_rn_fast(lr.d.x), rcp_rn_fast(lr.d.y), rcp_rn_fast(lr.d.z));
-      const bool ok = recip_div_ok(lr.d.x) && recip_div_ok(lr.d.y) && recip_div_ok(lr.d.z) &&
-                      fabsf(lr.o.x) < 0x1p62f && fabsf(lr.o.y) < 0x1p62f && fabsf(lr.o.z) < 0x1p62f;
+      // the fast path's ranges (|d_k| in [2^-60, 2^60], |o_k| < 2^62), tested stricter on sums (a NaN or infinite
+      // component makes its sum fail; a sum within the bound bounds each term): three compares instead of nine and
+      // two scalar ands instead of eight (cornell-800 +1.9%, r05z7); a stricter test only sends more lanes to the
+      // IEEE path
+      const float dmin = fminf(fminf(fabsf(lr.d.x), fabsf(lr.d.y)), fabsf(lr.d.z));
+      const float dsum = (fabsf(lr.d.x) + fabsf(lr.d.y)) + fabsf(lr.d.z);
+      const float osum = (fabsf(lr.o.x) + fabsf(lr.o.y)) + fabsf(lr.o.z);
+      const bool ok = (dmin >= 0x1p-60f) & (dsum <= 0x1p60f) & (osum < 0x1p62f);
       fast = S.rect_fast && __ballot(!ok) == 0;
     }
     if (fast) {
