@@ -310,13 +310,17 @@ __device__ __forceinline__ T uload(const T* p) {
   }
 }
 
+// a wrapper op's kind (op.x holds (float)IO_TRANSLATE or (float)IO_ROTY, rtw_flatten.cpp) compared as bits: an
+// integer compare, which a kernel-uniform op does on the scalar unit (a float compare is a VALU op plus an exec and)
+__device__ __forceinline__ bool op_is(float x, uint32_t kind) { return __float_as_uint(x) == __float_as_uint((float)kind); }
+
 template <bool UNI = false>
 __device__ __forceinline__ Ray to_local(const DevInst* in, Ray r) {
   const uint32_t n = UNI ? uload(&in->nops) : in->nops;
   for (uint32_t k = 0; k < n; ++k) {
     const float4* opp = reinterpret_cast<const float4*>(in->op[k]);
     const float4 op = UNI ? uload(opp) : *opp;
-    if (op.x == (float)IO_TRANSLATE) {
+    if (op_is(op.x, IO_TRANSLATE)) {
       r.o = sub(r.o, mk(op.y, op.z, op.w));
     } else {
       const float s = op.y, c = op.z;
@@ -1251,7 +1255,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
   float4 op0 = make_float4(0.f, 0.f, 0.f, 0.f), op1 = op0;
   V3 d0 = wr.d, d1 = wr.d;  // the ray direction inside wrapper 0 (after op 0) and wrapper 1 (after ops 0, 1)
   auto apply_op = [](float4 op, Ray& r) {  // transformations.rs:23-28 / :115-135, as to_local
-    if (op.x == (float)IO_TRANSLATE) {
+    if (op_is(op.x, IO_TRANSLATE)) {
       r.o = sub(r.o, mk(op.y, op.z, op.w));
     } else {
       const float s = op.y, c = op.z;
@@ -1320,7 +1324,7 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
     face(h, wr.d, h.n);
   } else if ((FEAT & F_INST) && inst && short_chain) {  // unwind inner -> outer (transformations.rs:29-37, :137-147)
     auto unwind_op = [&](float4 op, V3 dk) {
-      if (op.x == (float)IO_TRANSLATE) {
+      if (op_is(op.x, IO_TRANSLATE)) {
         h.p = add(h.p, mk(op.y, op.z, op.w));
         face(h, dk, h.n);
       } else {
@@ -1338,10 +1342,10 @@ __device__ Rec hit_record(const DevScene& S, const Ray& wr, const Best& b, uint3
       V3 dk = wr.d;  // direction as seen inside wrapper k = after ops 0..k
       for (int q = 0; q <= k; ++q) {
         const float4 op = *reinterpret_cast<const float4*>(I->op[q]);
-        if (op.x == (float)IO_ROTY) dk = mk(op.z * dk.x - op.y * dk.z, dk.y, op.y * dk.x + op.z * dk.z);
+        if (op_is(op.x, IO_ROTY)) dk = mk(op.z * dk.x - op.y * dk.z, dk.y, op.y * dk.x + op.z * dk.z);
       }
       const float4 op = *reinterpret_cast<const float4*>(I->op[k]);
-      if (op.x == (float)IO_TRANSLATE) {
+      if (op_is(op.x, IO_TRANSLATE)) {
         h.p = add(h.p, mk(op.y, op.z, op.w));
         face(h, dk, h.n);
       } else {
