@@ -830,7 +830,26 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
     const uint4 G = uload(reinterpret_cast<const uint4*>(S.lgroups + g));  // (first, count, instance, kind)
     if (G.z != cur) {  // wave-uniform
       cur = G.z;
-      lr = cur ? to_local<true>(S.insts + cur, r) : r;
+      lr = r;
+      if (cur) {  // a Cuboid's rotate_y + translate: both ops' loads at once, one wait (to_local's ops in order;
+                  // cornell-800 +0.8%, r05z10)
+        const DevInst* I = S.insts + cur;
+        const uint32_t n = uload(&I->nops);
+        const float4 op0 = uload(reinterpret_cast<const float4*>(I->op[0]));
+        const float4 op1 = uload(reinterpret_cast<const float4*>(I->op[1]));
+        auto apply = [&](const float4& op) {
+          if (op_is(op.x, IO_TRANSLATE)) {
+            lr.o = sub(lr.o, mk(op.y, op.z, op.w));
+          } else {
+            const float sn = op.y, c = op.z;
+            lr.o = mk(c * lr.o.x - sn * lr.o.z, lr.o.y, sn * lr.o.x + c * lr.o.z);
+            lr.d = mk(c * lr.d.x - sn * lr.d.z, lr.d.y, sn * lr.d.x + c * lr.d.z);
+          }
+        };
+        if (n >= 1u) apply(op0);
+        if (n >= 2u) apply(op1);
+        for (uint32_t k = 2; k < n; ++k) apply(uload(reinterpret_cast<const float4*>(I->op[k])));
+      }
       y = mk(rcp_rn_fast(lr.d.x), rcp_rn_fast(lr.d.y), rcp_rn_fast(lr.d.z));
       // the fast path's ranges (|d_k| in [2^-60, 2^60], |o_k| < 2^62), tested stricter on sums (a NaN or infinite
       // component makes its sum fail; a sum within the bound bounds each term): three compares instead of nine and
