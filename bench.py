@@ -237,7 +237,13 @@ def main() -> int:
     ap.add_argument("--multi-device", type=int, default=0,
                     help="N > 0: one process renders each frame on N GPUs through rtw_render_multi "
                          "(C-ABI, RCCL send/recv gather to device 0, frame copied to the host)")
+    ap.add_argument("--diag-alias", action="store_true",
+                    help="diagnostic (never a measurement): --multi-device N on ONE physical GPU, the scene's N "
+                         "devices being logical ones (rtw_diag_alias_devices); needs RTW_RCCL_LIB pointing at an "
+                         "RCCL stand-in that allows it (tests/loopback_rccl), as real RCCL refuses shared-GPU cliques")
     args = ap.parse_args()
+    if args.diag_alias and not (args.multi_device > 1 and os.environ.get("RTW_RCCL_LIB")):
+        raise SystemExit("--diag-alias needs --multi-device N > 1 and RTW_RCCL_LIB set (tests/loopback_rccl)")
 
     import torch
     import torch.distributed as dist
@@ -245,7 +251,8 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    multi = resolve_gpus(args, world, torch.cuda.device_count())
+    # --diag-alias: the N devices are logical ones on device 0 (one visible GPU suffices)
+    multi = resolve_gpus(args, world, args.multi_device if args.diag_alias else torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dev_id = local % max(1, torch.cuda.device_count())
@@ -264,6 +271,8 @@ def main() -> int:
         spp = args.spp
     scene = rtw.Scene()
     cam, bg = scene.preset(scene_name, rtw.camera_aspect(w, h), seed=SCENE_SEED)
+    if args.diag_alias:
+        scene.diag_alias_devices(multi)
     scene.commit(device=-1 if multi else dev)
     rt = rtw.Raytracer(scene, cam, bg, w, h, spp, seed=RENDER_SEED)
 
@@ -409,7 +418,9 @@ def main() -> int:
     # every frame rendered so far is valid: no traversal guard tripped (raises otherwise)
     for d in (range(multi) if multi else [dev]):
         scene.render_status(d)
-    pk = scene.path_kernel_times(0 if multi else dev)
+    # every device's launches, read once (a read also forgets them: rtw_path_kernel_times)
+    pk_dev = {d: scene.path_kernel_times(d) for d in (range(multi) if multi else [dev])}
+    pk = pk_dev[0 if multi else dev]
     if not pk or len(pk) >= 64 or len(pk) % (args.steps * launches):
         raise SystemExit(f"path-kernel timings: got {len(pk)} for {args.steps} steps x {launches} calls "
                          "(ring of 64 overflowed or launches missing; lower --steps)")
@@ -468,7 +479,7 @@ def main() -> int:
         gms_m = float(np.mean([t[1] for t in timing_multi]))
         dk = []  # path-kernel ms per frame of every device (the library's events on that device's stream)
         for d in range(multi):
-            pkd = pk if d == 0 else scene.path_kernel_times(d)  # device 0's were read above
+            pkd = pk_dev[d]
             dk.append(round(float(sum(pkd)) / args.steps, 3) if pkd else None)
         km = [round(float(x), 3) for x in dms.mean(axis=0)]
         multi_gpu = {"device_kernel_ms_per_frame": dk, "device_render_ms_per_frame": km,
@@ -508,6 +519,7 @@ def main() -> int:
             "dtype": "f32",
             "data": "synthetic (seeded scene generator, scenes.rs restated; seed %d)" % SCENE_SEED,
             "config": {"workload": cfg_text, "backend": args.backend if world > 1 else ("rccl" if multi else None),
+                       "diag_alias_devices": multi if args.diag_alias else None,
                        "scene": scene_name, "width": w, "height": h, "spp": spp, "max_depth": 50,
                        "rays_per_frame": frame_rays, "paths_per_frame": w * h * spp, "tiles": nt,
                        "launches_per_frame": launches,

@@ -337,8 +337,9 @@ int rtw_scene_image(const rtw_scene* s, uint32_t k, const uint8_t** rgb8, uint32
  * Feature; selects the path-kernel variant), 10 Perlin tables, 11 stack bound of the sorted-push
  * walk (LDS-node kernels), 12 runs of the always list (one wrapper chain and one prim kind each: the
  * list-mode rect loop's program), 13 1 if every rect admits the list loop's fast path (|k| < 2^62,
- * ordered bounds).  3-13 are valid once rtw_scene_commit has flattened the scene (also when its upload
- * failed for lack of a device). */
+ * ordered bounds), 14 1 if the BVH holds sphere tests (their leaves are padded for origins within D0
+ * and farther origins take the far-origin walk), 15 that D0 in thousandths.  3-15 are
+ * valid once rtw_scene_commit has flattened the scene (also when its upload failed for lack of a device). */
 int64_t rtw_scene_info(const rtw_scene* s, int what);
 /* Introspection for the test harness: the flattened 4-wide BVH (DevNode4, 128 B each, breadth-first
  * numbered; csrc/rtw_device.hpp), valid once rtw_scene_commit has flattened the scene (also when its

@@ -589,6 +589,8 @@ int64_t rtw_scene_info(const rtw_scene* s, int what) {
     case 11: return (int64_t)sc.flat.stack_need4;
     case 12: return (int64_t)sc.flat.lgroups.size();
     case 13: return (int64_t)sc.flat.rect_fast;
+    case 14: return (int64_t)sc.flat.far_check;
+    case 15: return (int64_t)llround(1000.0 * (double)sc.flat.far_d0);
     case 4: return (int64_t)sc.flat.depth;
     case 5: return (int64_t)sc.flat.always.size();
     case 6: return (int64_t)sc.flat.insts.size();

@@ -200,7 +200,33 @@ struct DevScene {
                           // loop's fast path may divide by reciprocals and test bounds with med3 (trace_rect_list)
   uint32_t bvh_tri;       // every BVH leaf primitive is a triangle of instance tri_inst (the leaf fast path)
   uint32_t tri_inst;
+  // 1: the BVH holds sphere tests, and rays from far origins take the far-origin path (DevFar, trace_begin)
+  uint32_t far_check;
 };
+
+// The far-origin bound (rtw_flatten.cpp far_bound): the BVH's sphere leaves are padded for origins whose farthest
+// corner of the BVH box B is within D0 (D(o)² = sum over axes of (|o - mid| + half)² <= d2); a ray from farther
+// away first tests B grown by delta(D) = min(q D² + q0, s D + s0) + l D + l0 and, on a hit, walks the tree with
+// every box grown by delta(D) (trace_far).  Stored 256 B before the prim table (the kernel derives its address from
+// DevScene::prims at each use, so none of it occupies registers across the path loop).
+struct alignas(16) DevFar {
+  float mid[3], d2;
+  float half[3], q;
+  float lo[3], q0;
+  float hi[3], s;
+  float s0, l, l0;
+  uint32_t n_bvh;        // BVH primitives (prims[0 .. n_bvh)): the flat pass of trace_far
+  uint32_t nodes_back;   // bytes from the node table to the prim table (both in the scene block)
+  uint32_t pad0;
+  // the far-path queue of this device copy (set by the host when it allocates it): the path ids handed to the far-path
+  // kernel, capacity farq_cap; the count lives in the render counters ([28]; [29] is the far-path kernel's dispenser)
+  uint64_t farq;
+  uint64_t farq_cap;
+  uint64_t pad1;
+};
+static_assert(sizeof(DevFar) == 112, "DevFar must be 112 B");
+
+constexpr uint32_t DEVFAR_BACK = 256;  // prims - DEVFAR_BACK bytes = the DevFar record
 
 struct DevCamera {
   float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];

@@ -8,11 +8,22 @@
 // wrapper space (Translation/YRotation do not rescale the ray).  So the world's answer is
 // "smallest candidate t over all leaves, ties to the largest DFS key", which is a
 // commutative reduction any traversal order reproduces, provided culling never drops a
-// leaf whose candidate could win.  Culling is made conservative by padding every box
-// (pad_box) and by a relative slack on the best t in the kernel.  Primitives whose box
-// is huge next to the rest (the r = 1000 ground sphere, scenes.rs:74-78) are kept out of
-// the BVH and tested for every ray ("always" list): it keeps the tree tight and removes
-// the grazing-ray precision cases of a 1000-unit sphere from the culling argument.
+// leaf whose candidate could win.  Primitives whose box is huge next to the rest (the
+// r = 1000 ground sphere, scenes.rs:74-78) are kept out of the BVH and tested for every ray
+// ("always" list): it keeps the tree tight.
+//
+// Culling is conservative because every candidate hit point lies inside its leaf's box as padded here, and
+// the kernel's slab test covers [0, best t · (1 + 1e-5) + 1e-5]:
+//  * pad_box (1e-4 + 4e-5 · the box's largest |coordinate|) covers the rounding of the slab test, of the
+//    wrapper transforms and of the linear primitive tests (rects; triangles hit at a non-grazing angle);
+//  * the f32 sphere test (spherical.rs:26-44) is NOT local: hb² - a·c cancels, so a ray whose origin is
+//    |oc| from the centre "hits" at points up to R'(|oc|) = sqrt(r² + 37u(|oc|² + r²)) + u|oc| from it
+//    (u = 2^-24, the first-order bound derived in DESIGN.md §2; the spurious band grows with |oc|², a ray
+//    from inside the r = 1000 ground sphere hits a 0.2 ball 2.5 r from its centre).  far_bound() pads
+//    every sphere leaf (and sphere-bounded medium) for origins within D0 of every BVH point (D0 = the
+//    diagonal of the BVH's box B: any origin inside B, jumpy-balls' camera too), and the kernel sends
+//    rays from farther away (DevScene::far_*, trace_begin) through a walk whose boxes grow by the bound
+//    at their own distance, after one test of B grown the same way (most such rays miss it).
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -63,6 +74,75 @@ struct Leaf {
   Box wbox;
   float c[3];
 };
+
+// ---- the far-origin bound of the sphere test (header comment)
+constexpr double U24 = 0x1p-24;
+constexpr double KU = 40.0 * U24;  // 37u of the first-order bound, rounded up to cover second-order terms
+// R'(D) - r for a sphere of radius r (>= 0) and an origin at most D from its centre: an upper bound
+double sphere_reach(double D, double r) {
+  const double x = KU * (D * D + r * r);
+  const double q = r > 0.0 ? x / (2.0 * r) : INFINITY;  // sqrt(r² + x) - r <= x / 2r, and <= sqrt(x)
+  return std::min(q, sqrt(x)) + U24 * D;
+}
+// the linear terms for an origin D away from a scene whose coordinates are at most M (slab test, wrapper
+// transforms, rect hit points: a few roundings of |o| and |p| each)
+double linear_reach(double D, double M) { return 16.0 * U24 * (D + M); }
+// |r| of a leaf whose test is the quadratic sphere test, or -1
+float quad_radius(const DevPrim& p) {
+  const uint32_t t = p.type_inst & 0xffu;
+  if (t == PT_SPHERE || t == PT_MSPHERE) return fabsf(p.q2[2]);
+  if (t == PT_MEDIUM && p.q2[1] == 0.0f) return fabsf(p.q0[3]);  // a sphere boundary
+  return -1.0f;
+}
+
+// Pads the BVH's sphere leaves for near origins and fills Flat::far_* for the kernel's far-origin walk.
+// Knob RTW_FAR_D0 (tuning): D0 as a multiple of B's diagonal.
+void far_bound(std::vector<Leaf>& rest, Flat& f) {
+  f.far_check = 0;
+  Box B;
+  float rmin = INFINITY, rmax = 0.0f;
+  for (const Leaf& L : rest) {
+    B.grow(L.wbox);
+    const float r = quad_radius(L.p);
+    if (r >= 0.0f) { rmin = std::min(rmin, r); rmax = std::max(rmax, r); }
+  }
+  if (!(rmin <= rmax) || !B.valid()) return;  // no sphere in the BVH: pad_box's linear bound suffices
+  double scale = 1.0;
+  if (const char* e = tuning_env("RTW_FAR_D0")) scale = std::min(8.0, std::max(0.05, atof(e)));
+  double M = 0.0;
+  for (int a = 0; a < 3; ++a) M = std::max(M, (double)std::max(fabsf(B.lo[a]), fabsf(B.hi[a])));
+  const double D0 = scale * (double)B.diag();
+  // near origins: every sphere centre c lies in B, so |o - c| <= D(o) = the farthest corner of B <= D0
+  for (Leaf& L : rest) {
+    const float r = quad_radius(L.p);
+    if (r < 0.0f) continue;
+    const float e = (float)((sphere_reach(D0, r) + linear_reach(D0, M)) * 1.01);
+    for (int a = 0; a < 3; ++a) { L.wbox.lo[a] -= e; L.wbox.hi[a] += e; }
+  }
+  // far origins: delta(D) = min(q D² + q0, s D + s0) + l D + l0 bounds sphere_reach(D, r) + linear_reach(D, M)
+  // over r in [rmin, rmax] (KU/2 (D²/r + r) and sqrt(KU (D² + r²)) <= sqrt(KU) (D + r)); 1% up for the
+  // kernel's f32 evaluation
+  f.far_check = 1;
+  DevFar& F = f.far;
+  memset(&F, 0, sizeof F);
+  for (int a = 0; a < 3; ++a) {
+    F.mid[a] = 0.5f * (B.lo[a] + B.hi[a]);
+    // half extent rounded up, so |o - mid| + half >= the farthest corner's distance on this axis
+    F.half[a] = nextafterf(std::max(B.hi[a] - F.mid[a], F.mid[a] - B.lo[a]), INFINITY);
+    F.lo[a] = B.lo[a];
+    F.hi[a] = B.hi[a];
+  }
+  f.far_d0 = (float)D0;
+  F.d2 = (float)(D0 * D0 * (1.0 - 1e-5));  // rounded down: an origin near D0 takes the far path
+  const double up = 1.01;
+  F.q = rmin > 0.0f ? (float)(up * KU / (2.0 * rmin)) : INFINITY;
+  F.q0 = (float)(up * KU * rmax / 2.0);
+  F.s = (float)(up * sqrt(KU));
+  F.s0 = (float)(up * sqrt(KU) * rmax);
+  F.l = (float)(up * (16.0 + 1.0) * U24);
+  F.l0 = (float)(up * 16.0 * U24 * M);
+  F.n_bvh = (uint32_t)rest.size();  // (nodes_back: set at upload)
+}
 
 struct Builder {
   const Scene& s;
@@ -678,6 +758,7 @@ int flatten(Scene& s) {
       f.tri_inst = inst;
     }
   }
+  far_bound(rest, f);  // sphere leaves padded for near origins, the far-origin walk's bound (header)
   if (!rest.empty()) {
     uint32_t lg = 0;
     while ((1ull << lg) < rest.size()) ++lg;

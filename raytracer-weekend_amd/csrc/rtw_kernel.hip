@@ -55,6 +55,9 @@ namespace dev {
 #if defined(RTW_DIAG_ONE_TRIP) && !defined(RTW_ALLOW_NON_REFERENCE)
 #error "RTW_DIAG_ONE_TRIP changes the sampled distribution (not the reference's): diagnostic builds only"
 #endif
+#if defined(RTW_DIAG_FAR) && !defined(RTW_ALLOW_NON_REFERENCE)
+#error "RTW_DIAG_FAR removes parts of the far-origin walk (timing diagnostic): diagnostic builds only"
+#endif
 #if defined(RTW_DIAG_NO_STORE) && !defined(RTW_ALLOW_NON_REFERENCE)
 #error "RTW_DIAG_NO_STORE drops the sample stores (the image is not computed): diagnostic builds only"
 #endif
@@ -592,6 +595,8 @@ __device__ __forceinline__ void test_sphere32(const DevScene& S, uint32_t pi, fl
 // List-mode kernels (F_LIST): a winner whose t is NaN (an in-plane hit, see rect_list_test) is carried with best
 // t = +inf and this bit in its index (list worlds have few prims); trace_begin hands it on with t = NaN
 constexpr int32_t RECT_NAN_HIT = 0x40000000;
+// Best::prim of a segment a main path kernel hands to the far-path kernel (path_kernel DEFER / FARQ): a miss here
+constexpr int32_t FAR_HANDOFF = -3;
 
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
@@ -879,9 +884,118 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
   best.prim = nan_hit ? (bp & ~RECT_NAN_HIT) : bp;
 }
 
-template <bool COUNT, uint32_t FEAT>
-__device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
-                                            uint64_t seg) {
+// ---- far-origin rays (round 6; rtw_flatten.cpp's header)
+// The BVH's sphere leaves are padded for origins within D0 of every BVH point.  From farther away (a path bouncing
+// inside the r = 1000 ground sphere: ~5% of jumpy-balls' segments) the reference's f32 sphere test "hits" a sphere
+// up to delta(D) outside it (its cancellation grows with D²), and its flat list finds such a hit wherever it lies.
+// trace_begin tests the BVH box grown by delta(D) first -- almost every far ray misses it and skips the BVH -- and
+// the rest (~5e-5 of jumpy-balls' segments) walk the tree here with every box grown by delta(D): a plain stack walk
+// over the global f32 node table (order never changes the answer: closest t, ties to the larger key), the lane's
+// own LDS stack column as its stack (its main walk has not started), each hit leaf's primitives tested in turn.  A
+// push past the column (never for a tree whose stack bound fits it) sends the lane through every BVH primitive.
+// It runs in the far-path kernel (path_kernel FARQ) only: inlined into the main kernels, even never executed, its
+// code cost them 5-9% through register and SGPR pressure (profiles/r06/experiments).
+// The DevFar record, DEVFAR_BACK bytes before the prim table, re-derived at each use (the asm hides the pointer's
+// provenance): otherwise the compiler hoists its ~20 kernel-uniform values into SGPRs held across the whole path
+// loop, which spilled other SGPRs into VGPR lanes (v_readlane / v_writelane in the hot loop: jumpy-1080p -7%)
+__device__ __forceinline__ const DevFar* far_record(const DevScene& S) {
+  const char* p = reinterpret_cast<const char*>(S.prims);
+  asm volatile("" : "+s"(p));
+  return reinterpret_cast<const DevFar*>(p - DEVFAR_BACK);
+}
+__device__ __forceinline__ float far_inv(float d) {  // trace_run's reciprocal (culling only)
+  const float dd = fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d);
+  return __builtin_amdgcn_rcpf(dd);
+}
+template <bool COUNT, uint32_t FEAT, int STACK, int BLK, bool C16, int NCAP>
+__device__ void trace_far(const DevScene& S, const Ray& r, Best& b, float delta, uint16_t* stk16, int32_t* stk,
+                          uint32_t* cnt, uint64_t seg, uint32_t* err, const float4* lnodes) {
+  const DevFar* const FR = far_record(S);
+  // the f32 node table: the workgroup's LDS copy in the LDS-node kernels, else global memory
+  const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes)
+                                  : reinterpret_cast<const char*>(S.prims) - uload(&FR->nodes_back);
+  const uint32_t n_bvh = uload(&FR->n_bvh);
+  const V3 inv = mk(far_inv(r.d.x), far_inv(r.d.y), far_inv(r.d.z));
+  const V3 ood = mk(r.o.x * inv.x, r.o.y * inv.y, r.o.z * inv.z);
+  // every box grown by delta: its near plane delta |inv| earlier, its far plane delta |inv| later
+  const V3 bn = mk(-ood.x - delta * fabsf(inv.x), -ood.y - delta * fabsf(inv.y), -ood.z - delta * fabsf(inv.z));
+  const V3 bf = mk(-ood.x + delta * fabsf(inv.x), -ood.y + delta * fabsf(inv.y), -ood.z + delta * fabsf(inv.z));
+  const uint32_t nx = inv.x < 0.f ? 16u : 0u, ny = (inv.y < 0.f ? 16u : 0u) + 32u, nz = (inv.z < 0.f ? 16u : 0u) + 64u;
+  const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
+  int32_t node = 0, sp = 0;
+  bool over = false;
+  for (uint32_t guard = 0;; ++guard) {
+    if (node < 0) {
+      if (sp == 0) break;
+      --sp;
+      node = C16 ? (int32_t)stk16[sp * BLK] : stk[sp * BLK];
+    }
+    if (guard >= (1u << 20)) {  // a corrupt tree (cycle): end the walk and report, as trace_run does
+      *err = 1u;
+      b.prim = -2;
+      return;
+    }
+    if (COUNT) cnt[0]++;
+    const uint32_t nb = (uint32_t)node << 7;  // sizeof(DevNode4)
+    const float4 qnx = *reinterpret_cast<const float4*>(NB + (nb + nx)), qfx = *reinterpret_cast<const float4*>(NB + (nb + fx));
+    const float4 qny = *reinterpret_cast<const float4*>(NB + (nb + ny)), qfy = *reinterpret_cast<const float4*>(NB + (nb + fy));
+    const float4 qnz = *reinterpret_cast<const float4*>(NB + (nb + nz)), qfz = *reinterpret_cast<const float4*>(NB + (nb + fz));
+    // 16-bit codes (0 = empty) or the 32-bit child words (0 = empty: the root is nobody's child)
+    const uint4 cw = *reinterpret_cast<const uint4*>(NB + (nb + (C16 ? 112u : 96u)));
+    const float tmax_c = __builtin_fmaf(b.t, 1.0e-5f, b.t) + 1.0e-5f;
+    const float NX[4] = {qnx.x, qnx.y, qnx.z, qnx.w}, FX[4] = {qfx.x, qfx.y, qfx.z, qfx.w};
+    const float NY[4] = {qny.x, qny.y, qny.z, qny.w}, FY[4] = {qfy.x, qfy.y, qfy.z, qfy.w};
+    const float NZ[4] = {qnz.x, qnz.y, qnz.z, qnz.w}, FZ[4] = {qfz.x, qfz.y, qfz.z, qfz.w};
+    const uint32_t W[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t hits = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(NX[k], inv.x, bn.x), __builtin_fmaf(NY[k], inv.y, bn.y)),
+                                   __builtin_fmaf(NZ[k], inv.z, bn.z)), 0.0f);
+      const float tf = fminf(fminf(fminf(__builtin_fmaf(FX[k], inv.x, bf.x), __builtin_fmaf(FY[k], inv.y, bf.y)),
+                                   __builtin_fmaf(FZ[k], inv.z, bf.z)), tmax_c);
+      hits |= (W[k] != 0u && tn <= tf) ? 1u << k : 0u;
+    }
+    node = -1;
+    while (hits) {
+      const int k = __builtin_ctz(hits);
+      hits &= hits - 1u;
+      const uint32_t w = k == 0 ? W[0] : (k == 1 ? W[1] : (k == 2 ? W[2] : W[3]));
+      if (C16 ? (w & 0x8000u) != 0u : (int32_t)w < 0) {  // a leaf: its primitives now
+        const uint32_t v = C16 ? w & 0xFFFFu : ~w;
+        const uint32_t first = C16 ? (v >> 2) & 0x1FFFu : v >> 3, n = C16 ? (v & 3u) + 1u : v & 7u;
+        for (uint32_t q = 0; q < n; ++q) test_prim<COUNT, FEAT>(S, first + q, r, b, cnt, seg);
+      } else if (node < 0) {
+        node = (int32_t)w;
+      } else if (sp < STACK) {
+        if constexpr (C16) stk16[sp * BLK] = (uint16_t)w;
+        else stk[sp * BLK] = (int32_t)w;
+        ++sp;
+      } else {
+        over = true;  // the subtree is covered by the flat pass below
+      }
+    }
+  }
+  if (over)
+    for (uint32_t pi = 0; pi < n_bvh; ++pi) test_prim<COUNT, FEAT>(S, pi, r, b, cnt, seg);
+}
+
+// Kernel variants that carry the far-origin path: BVH walks that may test spheres.  Not the mesh kernels (F_MESHES):
+// a mesh world with spheres in its BVH (DevScene::far_check without bvh_tri) runs the generic kernel instead
+// (pick_kernel), since even unexecuted the far code cost cow-1080p 0.6% and monument-4k 0.3% (r06)
+constexpr bool far_kernel_feat(uint32_t feat) {
+  return !(feat & F_LIST) && (feat & (F_SPHERE | F_MSPHERE | F_MEDIUM)) && feat != F_MESHES;
+}
+// C16: the kernel's LDS stack holds 16-bit entries (the LDS-node and S16 walks), else 32-bit ones (stk); trace_far
+// borrows the lane's column.  Returns true for a lane whose segment needs the far-origin walk.  DEFER (the main path
+// kernels): such a lane does not take the walk here and the path kernel hands the path to the far-path kernel
+// (path_kernel FARQ), so the walk's code is not inlined into the hot kernels (inlined, it cost jumpy-1080p 5-9% by
+// register and SGPR pressure alone, profiles/r06/experiments)
+template <bool COUNT, uint32_t FEAT, int STACK = 1, int BLK = BLOCK, bool C16 = false, bool DEFER = false, int NCAP = 0>
+__device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
+                                            uint64_t seg, uint16_t* stk16 = nullptr, int32_t* stk = nullptr,
+                                            uint32_t* err = nullptr, const float4* lnodes = nullptr) {
+  bool deferred = false;
   ts.b = Best{INFINITY, 0u, -1, 0.0f, 0.0f};
   // list-mode worlds of rects only (the F_BOXES | F_LIST kernel)
   constexpr bool RECT_LIST = (FEAT & F_LIST) && (FEAT & F_RECT) && !(FEAT & (F_SPHERE | F_MSPHERE | F_TRI | F_MEDIUM));
@@ -918,6 +1032,57 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
     ts.b.t = nan_hit ? __builtin_nanf("") : ts.b.t;
     ts.b.prim = nan_hit ? (ts.b.prim & ~RECT_NAN_HIT) : ts.b.prim;
   }
+  // far-origin rays (above): the BVH box grown by delta(D) over [0, best], then trace_far for the few that reach it;
+  // neither takes the main walk
+  bool walk = true;
+#if defined(RTW_DIAG_FAR)  // timing diagnostic: 1 = no far check (pads only), 2 = far lanes skip the BVH, 3 = no far walk
+                          // (the slab test's result unused: removed), 5 = the slab test kept, no far walk
+  constexpr int DF = RTW_DIAG_FAR;
+#else
+  constexpr int DF = 0;
+#endif
+  constexpr bool FAR = DF != 1 && far_kernel_feat(FEAT);
+  if constexpr (FAR) {
+    if (S.far_check) {  // kernel-uniform
+      const float4* const FR = reinterpret_cast<const float4*>(far_record(S));
+      const float4 mid = uload(FR), half = uload(FR + 1);  // (mid, d2), (half, q)
+      const float tx = fabsf(r.o.x - mid.x) + half.x;
+      const float ty = fabsf(r.o.y - mid.y) + half.y;
+      const float tz = fabsf(r.o.z - mid.z) + half.z;
+      const float D2 = tx * tx + ty * ty + tz * tz;  // the farthest corner of the BVH box, squared
+      const bool far = D2 > mid.w;
+      if (__any(far)) {
+        bool need = false;
+        float delta = 0.0f;
+        if (far && DF != 2) {
+          const float4 lo = uload(FR + 2), hi = uload(FR + 3), e = uload(FR + 4);  // (lo, q0), (hi, s), (s0, l, l0)
+          // D from v_sqrt_f32 (1 ulp) rounded up; delta grows with D
+          const float D = __builtin_amdgcn_sqrtf(D2) * 1.000001f;
+          delta = fminf(half.w * D2 + lo.w, hi.w * D + e.x) + (e.y * D + e.z);
+          // the BVH box grown by delta, centred: |p - mid| <= half + delta per axis, over [0, best].  Raw reciprocals:
+          // a zero direction component gives +-inf planes (the axis unconstrained, or a miss), and a NaN (0 * inf: the
+          // origin exactly on a grown plane, the ray in it) drops out of fminf / fmaxf as a miss -- correct, since the
+          // spurious-hit region lies strictly inside the grown box (delta has 1% to spare)
+          const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y), iz = __builtin_amdgcn_rcpf(r.d.z);
+          const float ox = r.o.x - mid.x, oy = r.o.y - mid.y, oz = r.o.z - mid.z;
+          const float hx = half.x + delta, hy = half.y + delta, hz = half.z + delta;
+          const float ax = (-hx - ox) * ix, bx = (hx - ox) * ix, ay = (-hy - oy) * iy, by = (hy - oy) * iy;
+          const float az = (-hz - oz) * iz, bz = (hz - oz) * iz;
+          const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+          const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)),
+                                 fminf(fmaxf(az, bz), __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f));
+          need = tn <= tf;
+        }
+        walk = !far;
+        if (DF == 5) asm volatile("" ::"v"((uint32_t)need));  // timing diagnostic: the test kept, no hand-off
+        deferred = need && DF != 3 && DF != 5;
+        if constexpr (!DEFER) {
+          if (__builtin_expect(__any(need), 0))
+            if (need) trace_far<COUNT, FEAT, STACK, BLK, C16, NCAP>(S, r, ts.b, delta, stk16, stk, cnt, seg, err, lnodes);
+        }
+      }
+    }
+  }
   // the root (or none) made opaque here: hoisted out of the path loop, the compiler kept it in a VGPR across the
   // whole loop and spilled it.  Triangle kernels (the mesh walk): as a scalar, since the 7-wave walk spilled even
   // the opaque VGPR copy to scratch (one reload per segment; s1)
@@ -928,10 +1093,11 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
   } else {
     asm volatile("" : "+v"(root));
   }
-  ts.node = root;
+  ts.node = walk ? root : -1;
   ts.pend = 0;
   ts.sp = 0;
   ts.on = true;
+  return deferred;
 }
 
 // while-while walk of the 4-wide BVH with postponed leaves (Aila & Laine 2009): phase 1 visits
@@ -1598,8 +1764,13 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
 
 // BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
+// FARQ: the far-path kernel.  The main kernels (FARQ = false) of worlds with sphere tests in the BVH hand every path
+// whose next segment needs the far-origin walk (trace_begin, trace_far) to a queue (its path id, DevFar::farq) and
+// take a new path; this kernel, launched after each main pass, replays those paths from their start (a path is a
+// function of its id: the same draws, the same hits) and runs them to the end with the walk inlined, counting only
+// the segments after the handed-over one.  Its speed hardly matters (jumpy-1080p: ~0.6 ms of a 110 ms frame).
 template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, bool HN = false,
-          bool S16 = false>
+          bool S16 = false, bool FARQ = false>
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void path_kernel(RenderArgs a) {
   // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included);
   // S16 (global nodes, 16-bit entries): STACK + 1 rows of 16 bits
@@ -1653,7 +1824,19 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   };
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
-  const uint64_t P = a.n_paths;
+  // the far-path queue's count and this kernel's dispenser (counters [28], [29]), derived from the path queue's
+  // address where used (kernel arguments read in the loop are hoisted into SGPRs held across it)
+  auto farq_word = [&](int k) {
+    unsigned long long* q = a.queue;
+    asm volatile("" : "+s"(q));
+    return q - 3 + k;
+  };
+  constexpr bool DEFER = !FARQ && far_kernel_feat(FEAT);
+  const uint64_t P = FARQ ? *(volatile unsigned long long*)farq_word(0) : a.n_paths;
+  unsigned long long* const dispenser = FARQ ? farq_word(1) : a.queue;
+  // FARQ: the lane replays a handed-over path; its segments up to and including the one that needs the far walk (the
+  // first such) were counted by the main kernel
+  bool replay = false;
   uint32_t cnt[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
@@ -1698,7 +1881,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       if (avail < n_need) {  // refill: one atomic per BATCH paths
         // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        if (lane == 0) pool[2] = atomicAdd(a.queue, (unsigned long long)a.batch);
+        if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)a.batch);
         const uint64_t b = rfl64(pool[2]);
         if (b < P) {
           nb = b;
@@ -1710,7 +1893,17 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, id, st, stk16)) has = true;
+        if constexpr (FARQ) {  // replay a handed-over path from its start (its id in the queue)
+          if (rank < avail || id < ne) {
+            const uint32_t pid = reinterpret_cast<const uint32_t*>(far_record(S)->farq)[id];
+            if (start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, pid, st, stk16)) {
+              has = true;
+              replay = true;
+            }
+          }
+        } else if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, id, st, stk16)) {
+          has = true;
+        }
       }
       if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
       if (avail >= n_need) {
@@ -1729,10 +1922,18 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     phase(0);
     // segments starting now, counted per wave with every lane active (so the count is uniform
     // and stays in SGPRs)
-    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
+    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on && !replay));
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
-    if (!ts.on) trace_begin<COUNT, FEAT>(S, st.ray, ts, cnt, st.rng);
+    if (!ts.on) {
+      const bool far = trace_begin<COUNT, FEAT, STACK, BLK, (NCAP > 0 || S16), DEFER, (HN ? 0 : NCAP)>(
+          S, st.ray, ts, cnt, st.rng, stk16, stk, a.err, nodes_lds);
+      // DEFER: the segment needs the far-origin walk: it ends as a "miss" here (the hit record's prim FAR_HANDOFF, no
+      // walk) and the miss branch hands the path to the far-path kernel, whose replay overwrites its sample.  (Leaving
+      // the loop body early instead -- a `continue` -- cost the hot loop 5% through the control-flow structurizer.)
+      if constexpr (DEFER) ts.b.prim = far ? FAR_HANDOFF : ts.b.prim;
+      if constexpr (FARQ) replay = replay && !far;  // from the next segment on, the replay's segments count
+    }
     if (!(FEAT & F_LIST)) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
       const uint32_t quota = (act * a.quota16 + 15u) >> 4;
@@ -1767,11 +1968,17 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     if (b.prim < 0) {  // lib.rs:102-105
       L = mul(path_T(), bg);
       done = true;
+      if constexpr (DEFER) {
+        if (__builtin_expect(b.prim == FAR_HANDOFF, 0)) {  // hand the path (its id) to the far-path kernel
+          const unsigned long long slot = atomicAdd(farq_word(0), 1ull);  // (the host sizes the queue for every path)
+          reinterpret_cast<uint32_t*>(far_record(S)->farq)[slot] = LST ? lst_ld(4) : st.pid;
+        }
+      }
       if (__builtin_expect(b.prim == -2, 0)) {
         // trace_run tripped its guard (a corrupt tree; the frame is invalid and reported): close the path queue
         // for every wave and empty this wave's id pool, so the grid drains after about one trip per wave
         // instead of one per 64 paths (a trip is 2^20 node-loop iterations)
-        atomicMax(a.queue, (unsigned long long)P);
+        atomicMax(dispenser, (unsigned long long)P);
         pool[0] = pool[1];
       }
     } else {
@@ -2090,7 +2297,12 @@ int upload(Scene& s, int device) {
   if (device >= nlog) return fail(RTW_EINVAL, "device %d >= device count %d", device, nlog);
   const Flat& f = s.flat;
   std::vector<uint8_t> blob;
-  size_t o_nodes = put(blob, f.nodes4), o_prims = put(blob, f.prims), o_always = put(blob, f.always);
+  // the far-origin record sits DEVFAR_BACK bytes before the prim table (trace_begin derives it from S.prims)
+  DevFar far = f.far;
+  const size_t o_nodes = put(blob, f.nodes4), o_far = put(blob, std::vector<DevFar>{far});
+  size_t o_prims = put(blob, f.prims), o_always = put(blob, f.always);
+  if (o_prims - o_far != DEVFAR_BACK) return fail(RTW_EINVAL, "internal: far record not %u B before the prims", DEVFAR_BACK);
+  reinterpret_cast<DevFar*>(blob.data() + o_far)->nodes_back = (uint32_t)(o_prims - o_nodes);
   size_t o_tsh = put(blob, f.tshade), o_inst = put(blob, f.insts), o_mat = put(blob, f.mats);
   size_t o_tex = put(blob, f.texs), o_texel = put(blob, f.texels), o_perlin = put(blob, f.perlins);
   size_t o_shade = put(blob, f.shade), o_hnodes = put(blob, f.nodes4h), o_groups = put(blob, f.lgroups);
@@ -2116,6 +2328,7 @@ int upload(Scene& s, int device) {
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.hnodes = f.nodes4h.empty() ? nullptr : (const DevNode4h*)(base + o_hnodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
+    c.far_dev = base + o_far;
     c.scene.always = (const uint32_t*)(base + o_always);
     c.scene.tshade = (const DevTriShade*)(base + o_tsh);
     c.scene.insts = (const DevInst*)(base + o_inst);
@@ -2136,6 +2349,7 @@ int upload(Scene& s, int device) {
     c.scene.tri_inst = f.tri_inst;
     c.scene.rect_fast = f.rect_fast;
     memcpy(c.scene.uni_off, f.uni_off, sizeof f.uni_off);
+    c.scene.far_check = f.far_check;
     s.dev.push_back(c);
   }
   hipSetDevice(prev);
@@ -2156,7 +2370,7 @@ void release(Scene& s) {
     if (c.err_host) hipHostFree(c.err_host);
     if (c.sbuf) hipFree(c.sbuf);
     if (c.spill) hipFree(c.spill);
-    for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids}) free_buf(*b);
+    for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids, &c.farq}) free_buf(*b);
     for (void* e : c.ev)
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
     for (void* e : c.gev)
@@ -2207,7 +2421,7 @@ static uint64_t max_pass_paths() {
 
 template <bool C>
 static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_nodes, uint32_t need4,
-                           bool codes16, bool has_half) {
+                           bool codes16, bool has_half, bool far) {
   using namespace dev;
   if (env_int("RTW_STACK_LDS", 0) == 4) return {path_kernel<C, 4, true, 4, F_ALL>, 4u};  // spill-path test
   const bool sph = (feat & ~F_SPHERES) == 0;
@@ -2280,22 +2494,35 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
         // a partial LDS node cache (the top 128 / 376 / 760 node4s, the rest from global memory, sorted-push
         // walk) measured slower on cow / monument (profiles/r02/experiments, n7): the full-table kernels
         // are for trees that fit
+        if (far) return pick5<C, F_ALL>(need);  // spheres in a mesh world's BVH: the mesh kernels have no far path
         return pick_mesh(C, need, half, codes16);
       }
       return pick5<C, F_ALL>(need);
   }
 }
+// the far-path kernel (path_kernel FARQ), run after each main pass of a world whose BVH holds sphere tests
+// (DevScene::far_check): the main kernel's own LDS-node form for the default sphere kernel (a handed-over path replays
+// up to 50 segments one after another, so the far pass lasts about one path's latency: 2.1 ms per jumpy-1080p frame
+// with the generic kernel's global node reads, r06), else the generic all-features walk with the HBM stack spill
+static Variant far_kernel_variant(bool count, const Variant& main) {
+  using namespace dev;
+  if (main.k16 && main.block == 1024u && main.stack == 16u)
+    return count ? Variant{path_kernel<true, 16, false, 8, F_SPHERES, 1024, 144, false, false, true>, 16u, 1024u, true}
+                 : Variant{path_kernel<false, 16, false, 8, F_SPHERES, 1024, 144, false, false, true>, 16u, 1024u, true};
+  return count ? Variant{path_kernel<true, STACK_DEEP5, true, 5, F_ALL, BLOCK, 0, false, false, true>, (uint32_t)STACK_DEEP5}
+               : Variant{path_kernel<false, STACK_DEEP5, true, 5, F_ALL, BLOCK, 0, false, false, true>, (uint32_t)STACK_DEEP5};
+}
 static Variant path_kernel_variant(bool count, const Flat& f) {
   const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
   const bool list = f.nodes4.empty();
   const bool hh = f.codes16 && !f.nodes4h.empty();
-  return count ? pick_kernel<true>(feat, need, list, nn, need4, f.codes16, hh)
-               : pick_kernel<false>(feat, need, list, nn, need4, f.codes16, hh);
+  return count ? pick_kernel<true>(feat, need, list, nn, need4, f.codes16, hh, f.far_check != 0)
+               : pick_kernel<false>(feat, need, list, nn, need4, f.codes16, hh, f.far_check != 0);
 }
 
-static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
-  int& g = c.grid[count ? 1 : 0];
-  void*& gf = c.grid_fn[count ? 1 : 0];
+static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count, bool farq = false) {
+  int& g = c.grid[(count ? 1 : 0) + (farq ? 2 : 0)];
+  void*& gf = c.grid_fn[(count ? 1 : 0) + (farq ? 2 : 0)];
   if (g > 0 && gf == (void*)fn) return g;
   gf = (void*)fn;
   int per_cu = 0, cus = 0;
@@ -2395,6 +2622,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
   } else if (n_slots) {
     const uint64_t per_slot = 64ull * spp;
+    const bool farq = sc.flat.far_check != 0;
     const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, max_pass_paths() / per_slot);
     const uint64_t need = std::min<uint64_t>(n_slots, slots_per_pass) * per_slot;
     if (need > c.sbuf_paths) {  // grow the ordered sample buffer (first render only)
@@ -2449,6 +2677,36 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       c.spill_bytes = spill_bytes;
     }
     a.spill = c.spill;
+    // the far-path kernel: its own grid and spill rows (it shares the spill area: it runs after the main pass), and the
+    // queue, room for every path id of a pass (4 B each: 4.2 GB at jumpy-1080p x 512), whose address the device's
+    // DevFar record holds
+    RenderArgs af = a;
+    Variant fvar{};
+    int fgrid = 0;
+    if (farq) {
+      fvar = far_kernel_variant(count, var);
+      fgrid = resident_grid(c, fvar.fn, fvar.block, count, true);
+      af.spill_depth = (!fvar.k16 && sc.flat.stack_need > fvar.stack) ? sc.flat.stack_need - fvar.stack : 0;
+      af.spill_lanes = (uint32_t)fgrid * fvar.block;
+      af.batch = 64;
+      const size_t fbytes = (size_t)af.spill_depth * af.spill_lanes * sizeof(int32_t);
+      if (fbytes > c.spill_bytes) {
+        if (c.spill) HIPCHK(hipFree(c.spill), "hipFree(stack spill)");
+        c.spill = nullptr;
+        c.spill_bytes = 0;
+        HIPCHK(hipMalloc((void**)&c.spill, fbytes), "hipMalloc(stack spill)");
+        c.spill_bytes = fbytes;
+      }
+      a.spill = af.spill = c.spill;
+      const uint64_t cap = need;  // paths of the largest pass
+      if (cap * sizeof(uint32_t) > c.farq.cap) {
+        HIPCHK(hipStreamSynchronize(stream), "hipStreamSynchronize");  // an earlier render may still read the queue
+        if (int e = grow(c.farq, cap * sizeof(uint32_t))) return e;
+        const uint64_t rec[2] = {(uint64_t)(uintptr_t)c.farq.p, cap};
+        HIPCHK(hipMemcpy(static_cast<char*>(c.far_dev) + offsetof(DevFar, farq), rec, sizeof rec, hipMemcpyHostToDevice),
+               "hipMemcpy(far queue)");
+      }
+    }
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
@@ -2456,13 +2714,20 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       a.batch = batch0;
       if (batch_auto)
         while (a.batch / 2u >= batch_floor && a.n_paths < (uint64_t)a.batch * waves * 32u) a.batch /= 2u;
-      if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
+      // the far-path queue's count and dispenser ([28], [29]) and the path queue ([31])
+      if (base) HIPCHK(hipMemsetAsync(a.queue - 3, 0, 4 * sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
       hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
       HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
       hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
       HIPCHK(hipGetLastError(), "path_kernel launch");
+      if (farq) {  // the paths the pass handed over (DevFar::farq), to the end; timed with the pass
+        af.slot_base = a.slot_base;
+        af.n_paths = a.n_paths;
+        hipLaunchKernelGGL(fvar.fn, dim3(fgrid), dim3(fvar.block), 0, stream, af);
+        HIPCHK(hipGetLastError(), "far-path kernel launch");
+      }
       HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
       c.kev_head = (c.kev_head + 1) % 64u;
       c.kev_count = std::min(c.kev_count + 1u, 64u);

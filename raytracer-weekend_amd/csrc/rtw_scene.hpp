@@ -80,6 +80,10 @@ struct Flat {
   uint32_t tri_inst = 0;
   float uni_off[3] = {0, 0, 0};
   float time_lo = 0.f, time_hi = 1.f;  // shutter interval the moving-sphere boxes cover
+  // the far-origin bound of the BVH's sphere tests (rtw_flatten.cpp far_bound; DevScene::far_*)
+  uint32_t far_check = 0;
+  DevFar far{};
+  float far_d0 = 0.f;
 };
 
 struct DevBuf {  // a grow-only device allocation
@@ -104,8 +108,10 @@ struct DeviceCopy {
   void* kev[64][2] = {};                   // hipEvent_t pairs around path-kernel launches (ring,
                                            // rtw_path_kernel_times)
   uint32_t kev_head = 0, kev_count = 0;
-  int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting) of the
-  void* grid_fn[2] = {nullptr, nullptr};   // variant it was computed for (knobs may switch variants)
+  int grid[4] = {0, 0, 0, 0};              // resident path_kernel grid (plain, counting; the far-path kernel's at
+  void* grid_fn[4] = {};                   // [2], [3]) of the variant it was computed for (knobs may switch variants)
+  DevBuf farq;                             // the far-path queue (path ids; DevFar::farq points here)
+  void* far_dev = nullptr;                 // the scene block's DevFar record on this device
   // device buffers kept across render calls (grown, never shrunk; freed by release()): a
   // 30-camera animation through rtw_render does no hipMalloc after the first frame
   DevBuf image, tiles, packed, gathered, gather_ids;

@@ -324,3 +324,39 @@ def test_list_runs_and_rect_fast_flag(rtw):
         s.xy_rect(bounds[0], bounds[1], bounds[2], bounds[3], k, m)
         _commit_anywhere(rtw, s)
         assert s.info(5) == 2 and s.info(12) == 1 and s.info(13) == 0
+
+
+def _sphere_reach(D, r):
+    """rtw_flatten.cpp sphere_reach: how far outside a radius-r sphere the reference's f32 test (spherical.rs:26-44)
+    can report a hit for an origin D from its centre (the first-order bound of DESIGN.md §2, 37u -> 40u)."""
+    ku = 40.0 * 2.0 ** -24
+    x = ku * (D * D + r * r)
+    return min(x / (2 * r), np.sqrt(x)) + 2.0 ** -24 * D
+
+
+def test_far_bound_pads_sphere_leaves(rtw):
+    """Round 6, VERDICT r5 item 1: a BVH holding spheres gets the far-origin bound (rtw_scene_info 14), with D0 the
+    diagonal of the BVH's box (info 15).  Every sphere leaf of jumpy-balls is padded by at least its reach at D0 (a
+    0.2 ball's leaf spans >= 2 (0.2 + reach)), so origins within D0 -- the camera and every bounce among the balls --
+    cull nothing the reference's flat list hits.  Worlds without BVH spheres (the cow's triangle-only tree, cornell's
+    list mode) need no bound."""
+    s = rtw.Scene()
+    s.preset("jumpy-balls", 16 / 9, seed=42)
+    _commit_anywhere(rtw, s)
+    assert s.info(14) == 1
+    d0 = s.info(15) / 1000.0
+    nd = s.nodes()
+    full = ~(nd["lo_x"] > nd["hi_x"])
+    lo = np.stack([nd["lo_" + a][0][full[0]].min() for a in "xyz"])
+    hi = np.stack([nd["hi_" + a][0][full[0]].max() for a in "xyz"])
+    diag = float(np.linalg.norm(hi - lo))
+    e = _sphere_reach(d0, 0.2)
+    assert 30.0 < d0 <= diag and d0 >= diag - 2 * np.sqrt(3) * (e + 1e-3), (d0, diag)
+    leaf = full & ((nd["code"] & 0x8000) != 0)
+    ext = np.stack([(nd["hi_" + a] - nd["lo_" + a])[leaf] for a in "xyz"]).min(axis=0)
+    assert ext.min() >= 2 * (0.2 + e), (ext.min(), e)
+    for name, aspect in (("wavefront-cow-obj", 16 / 9), ("cornell-box", 1.0)):
+        s = rtw.Scene()
+        s.preset(name, aspect, seed=42)
+        _commit_anywhere(rtw, s)
+        assert s.info(14) == 0, name

@@ -43,6 +43,7 @@ def _single_and_multi(rtw, name, aspect, n, w, h, spp, seed=5):
     ("jumpy-balls", 16 / 9, 72, 40, 3),       # ragged: 9 x 5 tiles, the last tile row half outside
     ("cornell-box", 1.0, 40, 40, 4),          # list mode
     ("wavefront-cow-obj", 16 / 9, 48, 27, 2),  # mesh kernel, half-precision nodes
+    ("textured-monument", 16 / 9, 64, 36, 1),  # configs[4]'s scene (its 8-way split), image texture
 ])
 def test_render_multi_equals_render(gpu, loopback, name, aspect, w, h, spp, n):
     rtw = gpu
@@ -102,3 +103,28 @@ def test_aliased_scene_renders_per_logical_device(gpu, loopback):
     assert np.array_equal(img.cpu().numpy().view(np.uint32), ref.view(np.uint32))
     for d in range(3):
         many.render_status(d)
+
+
+def test_bench_multi_device_branch_runs(gpu):
+    """bench.py's single-process N > 1 branch (rtw_render_multi, the driver's `--gpus 8` without a
+    launcher) executed end to end before the first real 8-GPU node runs it: configs[4]'s scene over 8 logical devices
+    of this GPU (--diag-alias, the loopback RCCL), 1 spp, as a fresh process.  The line must say n_gpus 8, carry eight
+    per-device path-kernel times (each device's launches read once) and a gathered frame equal to the single-device
+    render (--check-image)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, RTW_RCCL_LIB=str(LOOPBACK))
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--multi-device", "8", "--diag-alias", "--config",
+                        "monument-4k", "--spp", "1", "--steps", "2", "--warmup", "1", "--check-image",
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert any(x.get("check_image") is True for x in lines), r.stdout
+    d = lines[-1]
+    assert d["n_gpus"] == 8 and d["config"]["diag_alias_devices"] == 8
+    dk = d["multi_gpu"]["device_kernel_ms_per_frame"]
+    assert len(dk) == 8 and all(x is not None and x > 0 for x in dk), dk
+    assert len(d["multi_gpu"]["device_render_ms_per_frame"]) == 8
