@@ -925,7 +925,10 @@ static vec3 sample_ray_iter(ctx_t* c, ray r, draws* d, uint32_t depth) {
     T = vmul(T, sc.att);
     r = sc.out;
   }
-  return v3(0, 0, 0);
+  /* depth exhausted: sample_ray(.., 0) returns black (lib.rs:98-100), which every level above multiplies by its
+   * attenuation (lib.rs:109-116): T * 0, not a constant 0 -- a NaN or infinite throughput gives NaN, a negative
+   * one -0, as the recursion does (RECURSIVE above) */
+  return vmul(T, v3(0, 0, 0));
 }
 
 typedef struct {

@@ -2032,6 +2032,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 #ifdef RTW_SHADE_DIAG
       phase(8);
 #endif
+      V3 Tn = mk(0.f, 0.f, 0.f);  // the throughput after this segment (scattering materials)
       if (light) {  // emit, no scatter
         L = mul(path_T(), att);
         done = true;
@@ -2054,7 +2055,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
           if (cannot || reflectance(cos_t, r0) > gen_f32(st.rng)) dir = reflect(ud, h.n);
           else dir = refract(ud, h.n, ratio);
         }
-        const V3 T2 = mul(path_T(), att);  // x * 1.0f == x: the Dielectric's T is unchanged
+        const V3 Tp = path_T();
+        const V3 T2 = mul(Tp, att);  // x * 1.0f == x: the Dielectric's T is unchanged
+        // an absorbed Metal ray returns emitted() = black (material.rs:87, lib.rs:109-110), which the recursion's
+        // parents multiply by their attenuations: T * 0, not a constant 0 (NaN / inf throughputs propagate, a
+        // negative one gives -0; round 6, a fuzz world whose sphere uv was NaN)
+        if (done) L = mul(Tp, mk(0.f, 0.f, 0.f));
+        Tn = T2;
         if constexpr (LST) {
           lst_st(0, __float_as_uint(T2.x));
           lst_st(1, __float_as_uint(T2.y));
@@ -2068,7 +2075,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 #ifdef RTW_SHADE_DIAG
       phase(9);
 #endif
-      if (!done) {  // lib.rs:98-100: depth 0 returns black
+      if (!done) {  // lib.rs:98-100: depth 0 returns black, times the attenuations above it (T * 0, as above)
         if constexpr (LST) {
           const uint32_t d = lst_ld(3) - 1u;
           lst_st(3, d);
@@ -2076,6 +2083,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         } else {
           done = --st.depth == 0u;
         }
+        if (done) L = mul(Tn, mk(0.f, 0.f, 0.f));
       }
     }
     if (done) {

@@ -22,9 +22,11 @@ cull a hit by slab rounding: DESIGN.md §2's documented deviations), and a few r
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -81,12 +83,28 @@ def gpu_phase(cfgs, d: Path) -> None:
                          "bands_equal_whole_frame": bool(np.array_equal(band_px[rows].view(np.uint32),
                                                                         frame[rows].view(np.uint32)))})
             frame = frame[rows]
+        meta["frame_sha256"] = hashlib.sha256(np.ascontiguousarray(frame).tobytes()).hexdigest()
         np.save(d / f"{cfg}_gpu.npy", frame)
         (d / f"{cfg}_meta.json").write_text(json.dumps(meta))
         print(json.dumps(meta)[:300], flush=True)
 
 
-def oracle_phase(cfgs, d: Path, out: Path, threads: int) -> None:
+def recursive_check(o, orc, ocam, bg, w, h, spp, mode, g, rows, threads) -> dict:
+    """The frame's GPU sums against the literal recursion's association (emitted + a0 * (a1 * (...)), lib.rs:109-116)
+    over two bands from the middle of the frame (the top rows are often sky): rounding differences only."""
+    mid = (len(rows) // 2) // 8 * 8
+    rr = rows[mid:mid + 8 * REC_BANDS]
+    t0 = time.time()
+    rec, _ = o.render(ocam, bg, w, h, spp, seed=RENDER_SEED, threads=threads, integrator=orc.RECURSIVE,
+                      rows=[h - 1 - int(x) for x in rr], bvh_mode=mode)
+    ga, ra = g[mid:mid + len(rr)].astype(np.float64) / spp, rec[rr].astype(np.float64) / spp
+    return {"rows": [int(rr[0]), int(rr[-1])], "rmse_mean": float(np.sqrt(np.mean((ga - ra) ** 2))),
+            "max_abs_mean": float(np.abs(ga - ra).max()),
+            "max_rel_component": float(np.max(np.abs(ga - ra) / np.maximum(np.abs(ra), 1e-30))),
+            "oracle_s": round(time.time() - t0, 1)}
+
+
+def oracle_phase(cfgs, d: Path, out: Path, threads: int, recursive_only: bool = False) -> None:
     rtw = importlib.import_module("raytracer-weekend_amd")
     import oracle as orc
     res = {"seeds": {"scene": SCENE_SEED, "render": RENDER_SEED}, "threads": threads, "configs": []}
@@ -101,6 +119,14 @@ def oracle_phase(cfgs, d: Path, out: Path, threads: int) -> None:
         ocam = orc.camera_from_fields(cam.as_dict())
         rows = np.array(meta.get("rows", range(h)))
         mode = getattr(orc, "BVH_" + MODE[cfg])
+        if recursive_only:  # refresh only the recursive-association entry of an existing result
+            old = json.loads(out.read_text())
+            for c in old["configs"]:
+                if c["config"] == cfg:
+                    c["recursive"] = recursive_check(o, orc, ocam, bg, w, h, spp, mode, g, rows, threads)
+                    print(json.dumps(c["recursive"]), flush=True)
+            out.write_text(json.dumps(old, indent=1) + "\n")
+            continue
         t0 = time.time()
         ref, rays = o.render(ocam, bg, w, h, spp, seed=RENDER_SEED, threads=threads, rows=[h - 1 - int(r) for r in rows],
                              bvh_mode=mode)
@@ -117,6 +143,7 @@ def oracle_phase(cfgs, d: Path, out: Path, threads: int) -> None:
              "mismatching_pixels": int(bad.any(axis=2).sum()), "mismatching_components": int(bad.sum()),
              "rmse_mean": float(np.sqrt(np.mean((gf - rf) ** 2))), "max_abs_mean": float(np.abs(gf - rf).max()),
              "mismatch_first": np.argwhere(bad.any(axis=2))[:8].tolist(), "oracle_s": round(t_orc, 1)}
+        r["gpu_frame_sha256"] = hashlib.sha256(np.ascontiguousarray(g).tobytes()).hexdigest()
         if "bands_equal_whole_frame" in meta:
             r["bands_equal_whole_frame"] = meta["bands_equal_whole_frame"]
         if cfg in FLAT_ROWS:  # a few rows against the flat list as well, bit for bit
@@ -127,33 +154,48 @@ def oracle_phase(cfgs, d: Path, out: Path, threads: int) -> None:
             b1 = g[idx].view(np.uint32) != fl[fr].view(np.uint32)
             r["flat_list_rows"] = {"rows": fr, "pixels": len(fr) * w, "mismatching_pixels": int(b1.any(axis=2).sum()),
                                    "oracle_s": round(time.time() - t0, 1)}
-        mid = (len(rows) // 2) // 8 * 8  # bands from the middle of the frame (the top rows are often sky)
-        rr = rows[mid:mid + 8 * REC_BANDS]
-        t0 = time.time()
-        rec, _ = o.render(ocam, bg, w, h, spp, seed=RENDER_SEED, threads=threads, integrator=orc.RECURSIVE,
-                          rows=[h - 1 - int(x) for x in rr], bvh_mode=mode)
-        ga, ra = g[mid:mid + len(rr)].astype(np.float64) / spp, rec[rr].astype(np.float64) / spp
-        r["recursive"] = {"rows": len(rr), "rmse_mean": float(np.sqrt(np.mean((ga - ra) ** 2))),
-                          "max_abs_mean": float(np.abs(ga - ra).max()), "oracle_s": round(time.time() - t0, 1)}
+        r["recursive"] = recursive_check(o, orc, ocam, bg, w, h, spp, mode, g, rows, threads)
         print(json.dumps(r), flush=True)
         res["configs"].append(r)
         out.parent.mkdir(parents=True, exist_ok=True)
         out.write_text(json.dumps(res, indent=1) + "\n")
 
 
+def verify_phase(cfgs, out: Path) -> int:
+    """On the GPU box: re-render the configs with the current library and compare each frame's hash with the one the
+    oracle phase validated (profiles/r06/fullspp_parity.json), so a later build inherits the whole-frame result only
+    if it renders the same bits."""
+    res = json.loads(out.read_text())
+    known = {c["config"]: c for c in res["configs"]}
+    with tempfile.TemporaryDirectory() as t:
+        gpu_phase(cfgs, Path(t))
+        bad = 0
+        for cfg in cfgs:
+            meta = json.loads((Path(t) / f"{cfg}_meta.json").read_text())
+            same = known[cfg]["gpu_frame_sha256"] == meta["frame_sha256"] and \
+                known[cfg]["rays_gpu"] == meta.get("sample_rays_gpu", meta["frame_rays_gpu"])
+            print(json.dumps({"config": cfg, "lib_sha": meta["lib_sha"], "validated_lib_sha": known[cfg]["lib_sha"],
+                              "same_frame_and_rays": same}), flush=True)
+            bad += not same
+    return 1 if bad else 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--phase", choices=["gpu", "oracle"], required=True)
+    ap.add_argument("--phase", choices=["gpu", "oracle", "verify"], required=True)
     ap.add_argument("--configs", default="jumpy-1080p,cornell-800,cow-1080p,monument-4k")
     ap.add_argument("--dir", default="gpurun_out/fullspp")
     ap.add_argument("--out", default="profiles/r06/fullspp_parity.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    ap.add_argument("--recursive-only", action="store_true", help="refresh only the RECURSIVE comparison")
     a = ap.parse_args()
     cfgs = a.configs.split(",")
+    if a.phase == "verify":
+        return verify_phase(cfgs, Path(a.out))
     if a.phase == "gpu":
         gpu_phase(cfgs, Path(a.dir))
     else:
-        oracle_phase(cfgs, Path(a.dir), Path(a.out), a.threads)
+        oracle_phase(cfgs, Path(a.dir), Path(a.out), a.threads, a.recursive_only)
     return 0
 
 

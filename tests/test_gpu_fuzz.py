@@ -87,7 +87,7 @@ def test_random_world_bit_exact(gpu, orc, seed):
     _random_world(gpu, orc, seed, W, H, SPP)
 
 
-def _random_world(rtw, orc, seed, W, H, SPP):
+def _random_world(rtw, orc, seed, W, H, SPP, max_depth=50):
     rng = np.random.default_rng(1000 + seed)
     s = rtw.Scene()
     _build(rtw, s, rng)
@@ -97,12 +97,21 @@ def _random_world(rtw, orc, seed, W, H, SPP):
     bg = tuple(rng.uniform(0, 0.8, 3))
     text, imgs = s.dump(), s.images()
     s.commit()
-    g, st = rtw.Raytracer(s, cam, bg, W, H, SPP, seed=seed).render()
-    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, SPP, seed=seed)
+    g, st = rtw.Raytracer(s, cam, bg, W, H, SPP, seed=seed, max_depth=max_depth).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, SPP, seed=seed,
+                                                max_depth=max_depth)
     assert st["rays"] == rays, f"ray count {st['rays']} vs oracle {rays}"
     bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}: " \
                           f"gpu {g[tuple(bad[0][:2])]} oracle {r[tuple(bad[0][:2])]}"
+
+
+@pytest.mark.parametrize("max_depth", [50, 3])
+def test_nan_throughput_world_bit_exact(gpu, orc, max_depth):
+    """Round 6 (1,000 worlds at 96x54x8): world 329's UVDebug ground takes acos(-1.0000001) (spherical.rs:70-71), so
+    some paths carry a NaN throughput; a Metal that absorbs, or the depth limit, ends them with black times the
+    attenuations above (lib.rs:109-116): NaN, which the GPU once wrote as a constant 0."""
+    _random_world(gpu, orc, 329, 96, 54, 8, max_depth)
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("RTW_FUZZ_MESH_SEEDS", "6"))))

@@ -63,3 +63,37 @@ def test_estimator_converges(rtw, orc):
         b, _ = o.render(cam, bg, 16, 9, spp, seed=2)
         errs.append(np.sqrt(np.mean((a / spp - b / spp) ** 2)))
     assert errs[1] < errs[0] / 2
+
+
+def _fuzz_world(rtw, orc, seed, w, h):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    import test_gpu_fuzz as F  # the GPU fuzz suite's world builder (building needs no GPU)
+    rng = np.random.default_rng(1000 + seed)
+    s = rtw.Scene()
+    F._build(rtw, s, rng)
+    eye = rng.uniform(-1, 1, 3) * np.array([8, 2, 8]) + np.array([0, 3, 0])
+    cam = rtw.Camera.new(tuple(eye), tuple(rng.uniform(-1, 1, 3)), (0, 1, 0), float(rng.uniform(30, 70)), w / h,
+                         float(rng.choice([0.0, 0.1])), float(np.linalg.norm(eye)))
+    bg = tuple(rng.uniform(0, 0.8, 3))
+    return orc.OracleScene(s.dump(), s.images()), orc.camera_from_fields(cam.as_dict()), bg
+
+
+def test_nan_throughput_terminals_match_the_recursion(rtw, orc):
+    """Round 6: fuzz world 329 at 96x54x8 has paths whose throughput turns NaN (a UVDebug ground whose sphere uv
+    takes acos of -1.0000001, spherical.rs:70-71).  The recursion multiplies every terminal -- an absorbed Metal's
+    black, the black at depth 0 -- by the attenuations above it (lib.rs:109-116), so the NaN reaches the pixel; the
+    iterative form must return T * 0 there too, not a constant 0 (the GPU follows it: test_gpu_fuzz's regression)."""
+    o, cam, bg = _fuzz_world(rtw, orc, 329, 96, 54)
+    a, ra = o.render(cam, bg, 96, 54, 8, seed=329, integrator=orc.ITERATIVE)
+    b, rb = o.render(cam, bg, 96, 54, 8, seed=329, integrator=orc.RECURSIVE)
+    assert ra == rb
+    assert np.isnan(b).sum() > 0
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    ok = ~np.isnan(b)
+    assert np.allclose(a[ok], b[ok], rtol=2e-5, atol=1e-6)
+    # 20 paths deep at most: the depth-0 terminal of a NaN throughput too
+    a, _ = o.render(cam, bg, 96, 54, 8, seed=329, max_depth=3, integrator=orc.ITERATIVE)
+    b, _ = o.render(cam, bg, 96, 54, 8, seed=329, max_depth=3, integrator=orc.RECURSIVE)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
