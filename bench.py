@@ -433,7 +433,7 @@ def main() -> int:
 
     value = frame_rays * args.steps / dt / 1e6
     # HBM bytes per launch from the committed rocprofv3 PMC summary of this config (FETCH_SIZE x2 +
-    # WRITE_SIZE, separate passes; scripts/gpu_r04_evidence.sh + scripts/summarize_round.py), if any --
+    # WRITE_SIZE, separate passes; scripts/gpu_r05_evidence.sh + scripts/summarize_round.py), if any --
     # attached only when it was measured on THIS library build (its lib_sha stamp), else null + the reason
     sha = rtw.lib_sha()
     evidence_notes = []

@@ -25,6 +25,8 @@
 //    rays from farther away (DevScene::far_*, trace_begin) through a walk whose boxes grow by the bound
 //    at their own distance, after one test of B grown the same way (most such rays miss it).
 #include <math.h>
+
+#include <cmath>
 #include <stdlib.h>
 #include <string.h>
 
@@ -807,8 +809,11 @@ int flatten(Scene& s) {
   f.rect_fast = 1;
   for (const DevPrim& p : f.prims) {
     const uint32_t t = p.type_inst & 0xffu;
+    // (finite bounds too: x = o + t d can reach +-inf, and med3(inf, a0, inf) - inf is NaN, which the one-compare
+    // accept would then have to lose through fmaxf)
     if ((t == PT_RECT_XY || t == PT_RECT_XZ || t == PT_RECT_YZ) &&
-        !(fabsf(p.q1[0]) < 0x1p62f && p.q0[0] <= p.q0[1] && p.q0[2] <= p.q0[3]))
+        !(fabsf(p.q1[0]) < 0x1p62f && p.q0[0] <= p.q0[1] && p.q0[2] <= p.q0[3] && std::isfinite(p.q0[0]) &&
+          std::isfinite(p.q0[1]) && std::isfinite(p.q0[2]) && std::isfinite(p.q0[3])))
       f.rect_fast = 0;
   }
   // the always list as runs of one wrapper chain and one kind (DevScene::lgroups), in list order

@@ -2444,7 +2444,10 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
   // (no half-precision table when a bound is beyond f16's range: rtw_flatten.cpp half_node)
   const bool half = has_half && half_knob != 0;
   const bool half_lds = has_half && half_knob > 0;
-  if (list && !env_int("RTW_GENERIC", 0)) {
+  if (list) {
+    // RTW_GENERIC on a list world: the all-features LIST kernel, whose fold is the reference's (NaN candidates, list
+    // order); the BVH kernels' fold treats a NaN candidate as a miss
+    if (env_int("RTW_GENERIC", 0)) return {path_kernel<C, 1, false, 5, F_ALL | F_LIST>, 1u};
     // no BVH (list mode): variants without the walk.  The rect/instance one needs 56 VGPRs and
     // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
     // at 8; knob RTW_LIST_OCC); the all-features one spills below 96 VGPRs, so it stays at 5.

@@ -3,6 +3,7 @@
 # RTW_LANE_DIAG lane-state shares (lib/ab/lanediag, built by `bash scripts/ab_flags.sh lanediag -DRTW_LANE_DIAG`).
 #   usage: TAG=ls_ CONFIGS="jumpy-1080p" QS="1 2 4 8 12 16" bash scripts/gpu_lane_sweep.sh
 set -o pipefail
+export RTW_TUNING=1  # the library reads tuning knobs only with the gate open
 R=$GRAFT_REPO_ROOT
 TAG=${TAG:-ls_}
 mkdir -p $R/gpurun_out

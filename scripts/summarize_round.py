@@ -98,7 +98,7 @@ def main():
                 if "TCP_PENDING_STALL_CYCLES_sum" in c and c.get("GRBM_GUI_ACTIVE") else None,
                 "vmem_rd_per_ray": round(c["SQ_INSTS_VMEM_RD"] * 64 / rays, 3) if c.get("SQ_INSTS_VMEM_RD") and rays else None,
                 "counters": {k: round(v) for k, v in sorted(c.items())},
-                "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r04_evidence.sh)",
+                "source": f"{d.relative_to(ROOT)}/sq*_counter_collection.csv (scripts/gpu_r05_evidence.sh)",
                 "lib_sha": sha}
         (ROOT / "profiles" / f"valu_{cfg}.json").write_text(json.dumps(valu, indent=1))
         print(cfg, "pmc", pub["hbm_bytes_per_launch"], "valu_busy", valu["valu_busy"], "lane", valu["valu_lane_util"])

@@ -312,12 +312,13 @@ def test_list_runs_and_rect_fast_flag(rtw):
     """The list-mode rect loop's program (DevScene::lgroups, rtw_scene_info 12): cornell-box's 18 always-tested
     rects form 5 runs of one wrapper chain, in list order (the room's yz yz | xz xz xz | xy, then each box's
     xy xy xz xz yz yz as one whole-Cuboid run, GK_BOX6); its fast path (info 13) needs |k| < 2^62 and ordered bounds on every rect,
-    which a plane at 1e19 or an inverted rect revokes."""
+    which a plane at 1e19, an inverted rect or an infinite bound revokes."""
     s = rtw.Scene()
     s.preset("cornell-box", 1.0, seed=3)
     _commit_anywhere(rtw, s)
     assert (s.info(5), s.info(12), s.info(13)) == (18, 5, 1)
-    for k, bounds in ((1e19, (0.0, 1.0, 0.0, 1.0)), (1.0, (1.0, 0.0, 0.0, 1.0))):
+    for k, bounds in ((1e19, (0.0, 1.0, 0.0, 1.0)), (1.0, (1.0, 0.0, 0.0, 1.0)), (1.0, (0.0, float("inf"), 0.0, 1.0)),
+                      (1.0, (0.0, 1.0, float("-inf"), 1.0))):  # (infinite bounds: ADVICE r5)
         s = rtw.Scene()
         m = s.lambertian_solid((0.5, 0.5, 0.5))
         s.xy_rect(0.0, 1.0, 0.0, 1.0, 0.0, m)

@@ -152,7 +152,10 @@ def test_scheduling_knobs_bit_exact(gpu, orc, knobs, knob):
     Same for the node table in LDS vs global memory (RTW_LDS_NODES) and the occupancy variants
     (RTW_OCC).  Same for list mode vs BVH (RTW_LIST_MAX) and for other trees over the same prims (RTW_BVH_PAIR,
     RTW_BVH_BINS): closest hit with ties to the later object is a commutative reduction over the leaves,
-    whatever culls them."""
+    whatever culls them -- with one documented exemption: RTW_LIST_MAX=0 walks a list world's rects
+    through a BVH, whose fold counts a NaN candidate (an in-plane bounce, t = 0/0) as a miss where the reference's
+    list order lets it win; these frames hold no in-plane bounce (cornell-800 x 32 holds two, pinned in list mode by
+    test_in_plane_bounce_list_mode)."""
     k, v = knob.split("=")
     knobs.setenv(k, v)
     # the half-node knobs matter for BVH worlds: jumpy-balls (LDS nodes) and the cow (global nodes)
@@ -195,7 +198,8 @@ def test_path_kernel_times(gpu):
 @pytest.mark.parametrize("name,aspect,w,h,spp", [SCENES[1], SCENES[2], SCENES[3], SCENES[5]])
 def test_generic_kernel_bit_exact(gpu, orc, knobs, name, aspect, w, h, spp):
     """Every scene normally runs the smallest specialised kernel variant covering its features
-    (F_SPHERES / F_BOXES / F_MESHES, rtw_device.hpp); the all-features kernel must agree too."""
+    (F_SPHERES / F_BOXES / F_MESHES, rtw_device.hpp); the all-features kernel must agree too.  A list world
+    (cornell-box) takes the all-features LIST kernel, whose fold keeps the reference's NaN semantics."""
     knobs.setenv("RTW_GENERIC", "1")
     g, r, st, rays = _both(gpu, orc, name, aspect, w, h, spp)
     assert st["rays"] == rays

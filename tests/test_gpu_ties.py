@@ -171,7 +171,7 @@ def test_degenerate_primitives(gpu, orc):
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
 
 
-@pytest.mark.parametrize("kernel", ["rect_list", "all_features_list"])
+@pytest.mark.parametrize("kernel", ["rect_list", "all_features_list", "generic"])
 @pytest.mark.parametrize("tile,spp", [(2149, 20), (2347, 16)])
 def test_in_plane_bounce_list_mode(gpu, orc, knobs, kernel, tile, spp):
     """A Lambertian bounce off cornell's floor whose direction lost its normal component exactly (d.y = 0, the
@@ -181,11 +181,14 @@ def test_in_plane_bounce_list_mode(gpu, orc, knobs, kernel, tile, spp):
     loop reproduces this on its IEEE path.  These two tiles of the 800 x 800 bench frame (scene seed 42, render seed
     2024) hold the only two such events of its first 32 samples (scripts/count_bisect.py): their last sample is the
     one with the in-plane bounce.  Packed tile render against the oracle's rows, bit for bit, with ray counts; through
-    the rect list loop and through the all-features list kernel (knob RTW_LIST_ALL: test_prim's list fold)."""
+    the rect list loop and through the all-features list kernel (knob RTW_LIST_ALL: test_prim's list fold; and
+    RTW_GENERIC, which on a list world selects that same kernel: ADVICE r5)."""
     torch = pytest.importorskip("torch")
     rtw = gpu
     if kernel == "all_features_list":
         knobs.setenv("RTW_LIST_ALL", "1")
+    if kernel == "generic":
+        knobs.setenv("RTW_GENERIC", "1")
     w = h = 800
     s = rtw.Scene()
     cam, bg = s.preset("cornell-box", 1.0, seed=42)
