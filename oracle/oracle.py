@@ -55,6 +55,9 @@ def lib() -> C.CDLL:
             "oracle_render_counts": (C.c_int, [C.c_void_p, C.POINTER(oracle_camera), _F, C.c_uint32, C.c_uint32,
                                                C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_int, _U32,
                                                C.c_uint32, _F, C.POINTER(C.c_uint64), _U32]),
+            "oracle_render_pixels": (C.c_int, [C.c_void_p, C.POINTER(oracle_camera), _F, C.c_uint32, C.c_uint32,
+                                               C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_int, _U32,
+                                               C.c_uint32, _F, C.POINTER(C.c_uint64)]),
             "oracle_pcg32_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
             "oracle_rng_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, _U32, C.POINTER(C.c_uint64)]),
             "oracle_splitmix64": (C.c_uint64, [C.c_uint64]),
@@ -142,6 +145,20 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(lib().oracle_last_error().decode())
         return (out, int(rays.value), pr) if pixel_rays else (out, int(rays.value))
+
+    def render_pixels(self, cam: oracle_camera, background, w, h, spp, pixels, seed=0, max_depth=50,
+                      integrator=ITERATIVE, bvh_mode=BVH_AS_LIST, threads=None):
+        """-> (sums[n, 3], rays) of the given (j, i) pixels (j bottom-based), in their order."""
+        px = np.ascontiguousarray(np.asarray(pixels, np.uint32).reshape(-1, 2))
+        out = np.zeros((len(px), 3), np.float32)
+        rays = C.c_uint64()
+        n = threads or min(16, os.cpu_count() or 1)
+        rc = lib().oracle_render_pixels(self._p, C.byref(cam), fp(f32(background)), w, h, spp, max_depth, seed,
+                                        integrator, bvh_mode, n, px.ctypes.data_as(_U32), len(px), fp(out),
+                                        C.byref(rays))
+        if rc != 0:
+            raise RuntimeError(lib().oracle_last_error().decode())
+        return out, int(rays.value)
 
 
 def libm(fn: int, a, b=None) -> np.ndarray:

@@ -940,11 +940,31 @@ typedef struct {
   int integrator, bvh_mode;
   const uint32_t* rows;
   uint32_t n_rows;
+  const uint32_t* px; /* oracle_render_pixels: (j, i) pairs, one work item each; the sums go to out[k * 3] */
+  uint32_t n_px;
   float* out;
   uint32_t* pixel_rays;
   atomic_uint next;
   atomic_ullong rays;
 } job_t;
+
+/* one pixel's sum over its samples in sample order (lib.rs:78-95) */
+static vec3 render_pixel(job_t* jb, ctx_t* c, uint32_t j, uint32_t i, long tj, long ti, long ts) {
+  vec3 sum = v3(0, 0, 0);
+  for (uint32_t sidx = 0; sidx < jb->spp; ++sidx) {
+    draws d;
+    memset(&d, 0, sizeof d);
+    d.rng.s = oracle_path_state(jb->seed, j, i, sidx);
+    g_trace = (long)j == tj && (long)i == ti && (long)sidx == ts;
+    float u = ((float)i + gen_f32(&d)) / (float)(jb->w - 1u);
+    float v = ((float)j + gen_f32(&d)) / (float)(jb->h - 1u);
+    ray r = camera_get_ray(jb->cam, u, v, &d);
+    vec3 col = jb->integrator == ORACLE_RECURSIVE ? sample_ray_rec(c, &r, &d, jb->depth)
+                                                  : sample_ray_iter(c, r, &d, jb->depth);
+    sum = vadd(sum, col);
+  }
+  return sum;
+}
 
 static void* worker(void* arg) {
   job_t* jb = (job_t*)arg;
@@ -954,24 +974,18 @@ static void* worker(void* arg) {
   if (tr) sscanf(tr, "%ld,%ld,%ld", &tj, &ti, &ts);
   for (;;) {
     uint32_t k = atomic_fetch_add(&jb->next, 1u);
+    if (jb->px) {
+      if (k >= jb->n_px) break;
+      const vec3 sum = render_pixel(jb, &c, jb->px[2 * k], jb->px[2 * k + 1], tj, ti, ts);
+      float* o = jb->out + (size_t)k * 3;
+      o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
+      continue;
+    }
     if (k >= jb->n_rows) break;
     uint32_t j = jb->rows ? jb->rows[k] : (jb->h - 1u - k);
     for (uint32_t i = 0; i < jb->w; ++i) {
-      /* lib.rs:78-95 */
-      vec3 sum = v3(0, 0, 0);
       const uint64_t rays0 = c.rays;
-      for (uint32_t sidx = 0; sidx < jb->spp; ++sidx) {
-        draws d;
-        memset(&d, 0, sizeof d);
-        d.rng.s = oracle_path_state(jb->seed, j, i, sidx);
-        g_trace = (long)j == tj && (long)i == ti && (long)sidx == ts;
-        float u = ((float)i + gen_f32(&d)) / (float)(jb->w - 1u);
-        float v = ((float)j + gen_f32(&d)) / (float)(jb->h - 1u);
-        ray r = camera_get_ray(jb->cam, u, v, &d);
-        vec3 col = jb->integrator == ORACLE_RECURSIVE ? sample_ray_rec(&c, &r, &d, jb->depth)
-                                                      : sample_ray_iter(&c, r, &d, jb->depth);
-        sum = vadd(sum, col);
-      }
+      const vec3 sum = render_pixel(jb, &c, j, i, tj, ti, ts);
       float* o = jb->out + ((size_t)(jb->h - 1u - j) * jb->w + i) * 3;
       o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
       if (jb->pixel_rays) jb->pixel_rays[(size_t)(jb->h - 1u - j) * jb->w + i] = (uint32_t)(c.rays - rays0);
@@ -1002,6 +1016,34 @@ int oracle_render_counts(oracle_scene* s, const oracle_camera* cam, const float 
   jb.rows = rows; jb.n_rows = rows ? n_rows : h;
   jb.out = out;
   jb.pixel_rays = pixel_rays;
+  atomic_init(&jb.next, 0u);
+  atomic_init(&jb.rays, 0ull);
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  pthread_t th[256];
+  for (int t = 1; t < n_threads; ++t) pthread_create(&th[t], NULL, worker, &jb);
+  worker(&jb);
+  for (int t = 1; t < n_threads; ++t) pthread_join(th[t], NULL);
+  if (rays) *rays = atomic_load(&jb.rays);
+  return 0;
+}
+
+/* Selected pixels only: px = n_px (j, i) pairs (j bottom-based, as rows above); out[k * 3 ..] = pixel k's sums.
+ * (A full-spp frame's differing pixels re-rendered through another traversal mode, scripts/fullspp_parity.py.) */
+int oracle_render_pixels(oracle_scene* s, const oracle_camera* cam, const float background[3], uint32_t w,
+                         uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed, int integrator, int bvh_mode,
+                         int n_threads, const uint32_t* px, uint32_t n_px, float* out, uint64_t* rays) {
+  if (!s || !cam || !out || !px || w < 2 || h < 2) { set_err("bad arguments"); return -22; }
+  if (w > 65536 || h > 65536) { set_err("w, h <= 65536 (16-bit pixel coordinates in the path key)"); return -22; }
+  for (uint32_t k = 0; k < n_px; ++k)
+    if (px[2 * k] >= h || px[2 * k + 1] >= w) { set_err("pixel out of the frame"); return -22; }
+  job_t jb;
+  memset(&jb, 0, sizeof jb);
+  jb.s = s; jb.cam = cam; jb.bg = v3(background[0], background[1], background[2]);
+  jb.w = w; jb.h = h; jb.spp = spp; jb.depth = max_depth; jb.seed = seed;
+  jb.integrator = integrator; jb.bvh_mode = bvh_mode;
+  jb.px = px; jb.n_px = n_px;
+  jb.out = out;
   atomic_init(&jb.next, 0u);
   atomic_init(&jb.rays, 0ull);
   if (n_threads < 1) n_threads = 1;

@@ -62,6 +62,11 @@ int oracle_render_counts(oracle_scene* s, const oracle_camera* cam, const float 
                          uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
                          int integrator, int bvh_mode, int n_threads,
                          const uint32_t* rows, uint32_t n_rows, float* out, uint64_t* rays, uint32_t* pixel_rays);
+/* Selected pixels: px holds n_px (j, i) pairs (j bottom-based); out[k * 3 ..] receives pixel k's sums. */
+int oracle_render_pixels(oracle_scene* s, const oracle_camera* cam, const float background[3],
+                         uint32_t w, uint32_t h, uint32_t spp, uint32_t max_depth, uint64_t seed,
+                         int integrator, int bvh_mode, int n_threads,
+                         const uint32_t* px, uint32_t n_px, float* out, uint64_t* rays);
 
 /* ---- unit-level entry points used by the KAT / golden-vector tests ---- */
 uint32_t oracle_pcg32_stream(uint64_t state, uint32_t n, uint32_t* out, uint64_t* state_out);

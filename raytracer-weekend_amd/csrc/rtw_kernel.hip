@@ -948,15 +948,24 @@ __device__ void trace_far(const DevScene& S, const Ray& r, Best& b, float delta,
     const float NZ[4] = {qnz.x, qnz.y, qnz.z, qnz.w}, FZ[4] = {qfz.x, qfz.y, qfz.z, qfz.w};
     const uint32_t W[4] = {cw.x, cw.y, cw.z, cw.w};
     uint32_t hits = 0;
+    // the nearest internal child hit is walked next (the others pushed): the leaves met first shrink best t
+    float tnear = INFINITY;
+    int kn = -1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float tn = fmaxf(fmaxf(fmaxf(__builtin_fmaf(NX[k], inv.x, bn.x), __builtin_fmaf(NY[k], inv.y, bn.y)),
                                    __builtin_fmaf(NZ[k], inv.z, bn.z)), 0.0f);
       const float tf = fminf(fminf(fminf(__builtin_fmaf(FX[k], inv.x, bf.x), __builtin_fmaf(FY[k], inv.y, bf.y)),
                                    __builtin_fmaf(FZ[k], inv.z, bf.z)), tmax_c);
-      hits |= (W[k] != 0u && tn <= tf) ? 1u << k : 0u;
+      const bool h = W[k] != 0u && tn <= tf;
+      hits |= h ? 1u << k : 0u;
+      const bool inner = C16 ? (W[k] & 0x8000u) == 0u : (int32_t)W[k] >= 0;
+      const bool nearer = h && inner && tn < tnear;
+      tnear = nearer ? tn : tnear;
+      kn = nearer ? k : kn;
     }
-    node = -1;
+    node = kn < 0 ? -1 : (int32_t)(kn == 0 ? W[0] : (kn == 1 ? W[1] : (kn == 2 ? W[2] : W[3])));
+    hits &= kn < 0 ? hits : ~(1u << kn);
     while (hits) {
       const int k = __builtin_ctz(hits);
       hits &= hits - 1u;
@@ -965,8 +974,6 @@ __device__ void trace_far(const DevScene& S, const Ray& r, Best& b, float delta,
         const uint32_t v = C16 ? w & 0xFFFFu : ~w;
         const uint32_t first = C16 ? (v >> 2) & 0x1FFFu : v >> 3, n = C16 ? (v & 3u) + 1u : v & 7u;
         for (uint32_t q = 0; q < n; ++q) test_prim<COUNT, FEAT>(S, first + q, r, b, cnt, seg);
-      } else if (node < 0) {
-        node = (int32_t)w;
       } else if (sp < STACK) {
         if constexpr (C16) stk16[sp * BLK] = (uint16_t)w;
         else stk[sp * BLK] = (int32_t)w;
@@ -1834,6 +1841,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   constexpr bool DEFER = !FARQ && far_kernel_feat(FEAT);
   const uint64_t P = FARQ ? *(volatile unsigned long long*)farq_word(0) : a.n_paths;
   unsigned long long* const dispenser = FARQ ? farq_word(1) : a.queue;
+  // ids per dispenser atomic: the far-path kernel sizes it from the queued count (a.batch = 64 for the usual few
+  // thousand; ~32 batches per wave when a far camera hands over most of a frame's paths)
+  const uint32_t batch = FARQ ? (uint32_t)min(max(P / ((uint64_t)gridDim.x * (BLK / 64) * 32u), (uint64_t)a.batch), (uint64_t)1024)
+                              : a.batch;
   // FARQ: the lane replays a handed-over path; its segments up to and including the one that needs the far walk (the
   // first such) were counted by the main kernel
   bool replay = false;
@@ -1881,11 +1892,11 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       if (avail < n_need) {  // refill: one atomic per BATCH paths
         // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)a.batch);
+        if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
         const uint64_t b = rfl64(pool[2]);
         if (b < P) {
           nb = b;
-          ne = b + a.batch < P ? b + a.batch : P;
+          ne = b + batch < P ? b + batch : P;
         } else {
           exhausted = true;
         }
@@ -1970,8 +1981,16 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       done = true;
       if constexpr (DEFER) {
         if (__builtin_expect(b.prim == FAR_HANDOFF, 0)) {  // hand the path (its id) to the far-path kernel
-          const unsigned long long slot = atomicAdd(farq_word(0), 1ull);  // (the host sizes the queue for every path)
-          reinterpret_cast<uint32_t*>(far_record(S)->farq)[slot] = LST ? lst_ld(4) : st.pid;
+          // one atomic per wave (the handing-over lanes' count; the host sizes the queue for every path): per lane,
+          // a frame whose camera is far from the BVH (every path handed over) queued on the one counter word
+          const uint64_t m = __ballot(1);
+          const int lead = __builtin_ctzll(m);
+          unsigned long long base = 0;
+          if ((int)lane == lead) base = atomicAdd(farq_word(0), (unsigned long long)__popcll(m));
+          base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), lead) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, lead);
+          const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          reinterpret_cast<uint32_t*>(far_record(S)->farq)[base + rk] = LST ? lst_ld(4) : st.pid;
         }
       }
       if (__builtin_expect(b.prim == -2, 0)) {

@@ -154,6 +154,16 @@ def oracle_phase(cfgs, d: Path, out: Path, threads: int, recursive_only: bool = 
             b1 = g[idx].view(np.uint32) != fl[fr].view(np.uint32)
             r["flat_list_rows"] = {"rows": fr, "pixels": len(fr) * w, "mismatching_pixels": int(b1.any(axis=2).sum()),
                                    "oracle_s": round(time.time() - t0, 1)}
+        if MODE[cfg] == "REFERENCE" and bad.any():
+            # the pixels where the GPU and the reference's BvhNode tree differ, through the flat list (the GPU's set
+            # semantics): are they the tree's documented deviation (ties by tree position, slab-rounding culls)?
+            q = np.argwhere(bad.any(axis=2))
+            px = [(h - 1 - int(rows[a]), int(i)) for a, i in q]
+            t0 = time.time()
+            fl, _ = o.render_pixels(ocam, bg, w, h, spp, px, seed=RENDER_SEED, threads=threads)
+            b2 = g[q[:, 0], q[:, 1]].view(np.uint32) != fl.view(np.uint32)
+            r["differing_pixels_vs_flat_list"] = {"pixels": len(px), "mismatching_pixels": int(b2.any(axis=1).sum()),
+                                                  "oracle_s": round(time.time() - t0, 1)}
         r["recursive"] = recursive_check(o, orc, ocam, bg, w, h, spp, mode, g, rows, threads)
         print(json.dumps(r), flush=True)
         res["configs"].append(r)

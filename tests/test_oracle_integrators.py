@@ -54,6 +54,21 @@ def test_row_subset_matches_full(rtw, orc):
         assert np.array_equal(part[18 - 1 - j], full[18 - 1 - j])
 
 
+def test_pixel_subset_matches_full(rtw, orc):
+    """oracle_render_pixels (scripts/fullspp_parity.py re-renders a frame's differing pixels with it) gives each
+    pixel's sums of the whole-frame render, in the order asked, for both traversal modes."""
+    o, cam, bg = scene(rtw, orc, "wavefront-cow-obj")
+    px = [(17, 31), (0, 0), (9, 12), (9, 13), (4, 30)]  # (j bottom-based, i)
+    for mode in (orc.BVH_AS_LIST, orc.BVH_REFERENCE):
+        full, _ = o.render(cam, bg, 32, 18, 2, seed=8, bvh_mode=mode)
+        part, rays = o.render_pixels(cam, bg, 32, 18, 2, px, seed=8, bvh_mode=mode, threads=3)
+        assert rays > 0
+        for k, (j, i) in enumerate(px):
+            assert np.array_equal(part[k].view(np.uint32), full[18 - 1 - j, i].view(np.uint32))
+    with pytest.raises(RuntimeError):
+        o.render_pixels(cam, bg, 32, 18, 2, [(18, 0)])
+
+
 def test_estimator_converges(rtw, orc):
     """Different seeds estimate the same mean image: RMSE shrinks ~ 1/sqrt(spp)."""
     o, cam, bg = scene(rtw, orc, "cornell-box")
