@@ -1128,6 +1128,12 @@ __device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, Tra
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
 // HN: the walk reads the half-precision node table (DevNode4h: 4 loads / 64 B per visit instead of 7 / 112 B)
+#ifndef RTW_SRING
+#define RTW_SRING 1  // path starts made a ring of 64 at a time (path_kernel SRING; 0 = each lane's own, for A/B)
+#endif
+#ifndef REGEN_RING
+#define REGEN_RING 2  // regen_min of the kernels with the start ring
+#endif
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2_t as_h2(uint32_t u) { return __builtin_bit_cast(half2_t, u); }
 
@@ -1858,6 +1864,18 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // the sphere and list-mode kernels measured 0.5-1.4% slower with it, profiles/r05/experiments s1)
   uint64_t* const pool = pool_lds[S16 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
+  // SRING: the wave's ring of 64 path starts, made by all 64 lanes at once from 64 consecutive ids of its pool and
+  // taken by the lanes that regenerate (start_path is a function of the id alone, so which lane makes a path's start
+  // changes nothing).  start_path at full lane occupancy instead of the few idle lanes of each regeneration.
+  // Per lane slot: o, d, time, rng (2 words), pid (10 words, structure of arrays); rng = 0 marks an off-image id.
+  // (the rect list kernel only: its LDS is free and its VGPRs hold the generation; the LDS-node and mesh kernels have
+  // no LDS left for 2.5 KB per wave at their occupancy)
+  constexpr bool SRING = RTW_SRING && FEAT == (F_BOXES | F_LIST) && !FARQ && !LST;
+  __shared__ uint32_t ring_lds[SRING ? (BLK / 64) * 640 : 1];
+  __shared__ uint32_t ring_head_lds[SRING ? BLK / 64 : 1];
+  uint32_t* const ring = ring_lds + (SRING ? (threadIdx.x >> 6) * 640u : 0u);
+  uint32_t* const ring_head = ring_head_lds + (SRING ? threadIdx.x >> 6 : 0u);
+  if (SRING && lane == 0) ring_head[0] = 64u;
   bool exhausted = false;                // wave-uniform
   bool has = false;
   TraceState ts;
@@ -1882,7 +1900,65 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     phase(2);
     // ---- regeneration: compact new path ids into the idle lanes
     const uint64_t need = __ballot(!has);
-    if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
+    if constexpr (SRING) {
+      if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
+        const uint32_t n_need = (uint32_t)__popcll(need);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t head = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring_head[0]);
+        const uint32_t have = 64u - head;
+        auto take = [&](uint32_t e) {
+          const uint32_t lo = ring[7 * 64 + e], hi = ring[8 * 64 + e];
+          st.ray.o = mk(__uint_as_float(ring[e]), __uint_as_float(ring[64 + e]), __uint_as_float(ring[2 * 64 + e]));
+          st.ray.d = mk(__uint_as_float(ring[3 * 64 + e]), __uint_as_float(ring[4 * 64 + e]),
+                        __uint_as_float(ring[5 * 64 + e]));
+          st.ray.time = __uint_as_float(ring[6 * 64 + e]);
+          st.rng = ((uint64_t)hi << 32) | lo;
+          st.pid = ring[9 * 64 + e];
+          st.T = mk(1.f, 1.f, 1.f);
+          st.depth = SA.max_depth;
+          has = (lo | hi) != 0u;
+        };
+        const bool first = !has && rank < have;
+        if (first) take(head + rank);
+        if (n_need > have) {  // the ring is spent: 64 more starts from the pool (refilled by one atomic per batch)
+          uint64_t pool_next = rfl64(pool[0]), pool_end = rfl64(pool[1]);
+          if (pool_next >= pool_end) {
+            if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
+            const uint64_t b = rfl64(pool[2]);
+            pool_next = b < P ? b : P;
+            pool_end = b < P ? (b + batch < P ? b + batch : P) : P;
+          }
+          if (pool_next < pool_end) {  // pools and passes hold whole multiples of 64 ids
+            const uint64_t id = pool_next + lane;
+            PathState g;
+            const bool ok = start_path<SLDS, 0, 0, AB>(SA, id, g);
+            ring[lane] = __float_as_uint(g.ray.o.x);
+            ring[64 + lane] = __float_as_uint(g.ray.o.y);
+            ring[2 * 64 + lane] = __float_as_uint(g.ray.o.z);
+            ring[3 * 64 + lane] = __float_as_uint(g.ray.d.x);
+            ring[4 * 64 + lane] = __float_as_uint(g.ray.d.y);
+            ring[5 * 64 + lane] = __float_as_uint(g.ray.d.z);
+            ring[6 * 64 + lane] = __float_as_uint(g.ray.time);
+            ring[7 * 64 + lane] = ok ? (uint32_t)g.rng : 0u;
+            ring[8 * 64 + lane] = ok ? (uint32_t)(g.rng >> 32) : 0u;
+            ring[9 * 64 + lane] = (uint32_t)id;
+            pool_next += 64u;
+            if (!has && !first) take(rank - have);
+            head = n_need - have;
+          } else {
+            exhausted = true;  // no ids left: the ring stays empty
+            head = 64u;
+          }
+          if (lane == 0) { pool[0] = pool_next; pool[1] = pool_end; }
+        } else {
+          head += n_need;
+        }
+        if (lane == 0) ring_head[0] = head;
+        if (COUNT) ph[6] += __builtin_amdgcn_s_memtime() - t_sp;  // wave-uniform
+      }
+    } else if (need != 0 && !exhausted && ((uint32_t)__popcll(need) >= a.regen_min || need == __ballot(1))) {
       const uint32_t n_need = (uint32_t)__popcll(need);
       const uint32_t rank =
           __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -2247,6 +2323,7 @@ struct Variant {
   uint32_t stack;        // LDS stack rows of fn; a deeper push bound spills to HBM (RenderArgs::spill)
   uint32_t block = 256;  // workgroup size fn is compiled for
   bool k16 = false;      // LDS-node kernel (sorted-push walk)
+  bool sring = false;    // path starts from the wave's ring (path_kernel SRING)
 };
 // LDS-node variants: the node table lives in each workgroup's LDS.  512-lane workgroups at 6
 // waves/SIMD = 3 per CU: 24 rows of 16-bit stack entries x 512 x 2 B + 224 node4s x 128 B + the pool
@@ -2471,8 +2548,8 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
     // runs at 8 waves/SIMD (cornell-box on MI355X: 26.7k Mrays/s at 5-6 waves, 28.9k at 7, 29.5k
     // at 8; knob RTW_LIST_OCC); the all-features one spills below 96 VGPRs, so it stays at 5.
     if ((feat & ~F_BOXES) == 0 && !env_int("RTW_LIST_ALL", 0)) {  // knob: the all-features list kernel instead
-      if (env_int("RTW_LIST_OCC", 8) == 6) return {path_kernel<C, 1, false, 6, F_BOXES | F_LIST>, 1u};
-      return {path_kernel<C, 1, false, 8, F_BOXES | F_LIST>, 1u};
+      if (env_int("RTW_LIST_OCC", 8) == 6) return {path_kernel<C, 1, false, 6, F_BOXES | F_LIST>, 1u, 256u, false, RTW_SRING != 0};
+      return {path_kernel<C, 1, false, 8, F_BOXES | F_LIST>, 1u, 256u, false, RTW_SRING != 0};
     }
     return {path_kernel<C, 1, false, 5, F_ALL | F_LIST>, 1u};
   }
@@ -2680,8 +2757,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     // (RTW_REGEN_MIN sweep 1..32): 24 is best for open scenes (jumpy-balls +4.3%, cow +1.6%,
     // monument +1.7% over 1); closed boxes (cornell: 6.6 segments per path, few lanes finish per
     // iteration) lose with deep deferral: 8 (cornell list variant at 8 waves/SIMD: 29.3k at 1, 29.4k at 4, 29.8k at 8, 28.1k at 24).
+    // With the start ring (round 6, the rect list kernel) a regeneration costs a few LDS reads, not start_path at
+    // the idle lanes' occupancy, so waves refill early: REGEN_RING (cornell-800: 8 -> 2, +1.8%).
     const bool boxed = (sc.flat.features & ~F_SMOKE) == 0;
-    a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", boxed ? 8 : 24)));
+    a.regen_min = (uint32_t)std::min(64, std::max(1, env_int("RTW_REGEN_MIN", var.sring ? REGEN_RING : (boxed ? 8 : 24))));
     const int grid = resident_grid(c, fn, var.block, count);
     // Small frames: fewer ids per atomic, halving until every resident wave can take >= 32 batches.  configs[0]
     // (jumpy-balls 400x225x50: 4.5 M paths for 8,192 resident waves) handed out 4,395 batches of 1,024, so half the
