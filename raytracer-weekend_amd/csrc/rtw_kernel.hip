@@ -1128,6 +1128,9 @@ __device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, Tra
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
 // HN: the walk reads the half-precision node table (DevNode4h: 4 loads / 64 B per visit instead of 7 / 112 B)
+#ifndef RTW_FAR_INLINE
+#define RTW_FAR_INLINE 1  // the far-origin walk inlined into the main kernels; 0 = deferred to the far-path kernel (A/B)
+#endif
 #ifndef RTW_SRING
 #define RTW_SRING 1  // path starts made a ring of 64 at a time (path_kernel SRING; 0 = each lane's own, for A/B)
 #endif
@@ -1844,13 +1847,16 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     asm volatile("" : "+s"(q));
     return q - 3 + k;
   };
-  constexpr bool DEFER = !FARQ && far_kernel_feat(FEAT);
+  constexpr bool DEFER = !FARQ && far_kernel_feat(FEAT) && !RTW_FAR_INLINE;
   const uint64_t P = FARQ ? *(volatile unsigned long long*)farq_word(0) : a.n_paths;
   unsigned long long* const dispenser = FARQ ? farq_word(1) : a.queue;
   // ids per dispenser atomic: the far-path kernel sizes it from the queued count (a.batch = 64 for the usual few
   // thousand; ~32 batches per wave when a far camera hands over most of a frame's paths)
   const uint32_t batch = FARQ ? (uint32_t)min(max(P / ((uint64_t)gridDim.x * (BLK / 64) * 32u), (uint64_t)a.batch), (uint64_t)1024)
                               : a.batch;
+  // the far-path kernel's grid is the resident one, but its queue is usually a few thousand paths: the waves beyond
+  // the batches there are leave at once instead of each taking (and losing) a turn at the dispenser's atomic
+  if (FARQ && (uint64_t)(blockIdx.x * (BLK / 64) + (threadIdx.x >> 6)) * batch >= P) return;
   // FARQ: the lane replays a handed-over path; its segments up to and including the one that needs the far walk (the
   // first such) were counted by the main kernel
   bool replay = false;
@@ -2729,7 +2735,7 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
   } else if (n_slots) {
     const uint64_t per_slot = 64ull * spp;
-    const bool farq = sc.flat.far_check != 0;
+    const bool farq = sc.flat.far_check != 0 && !RTW_FAR_INLINE;
     const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, max_pass_paths() / per_slot);
     const uint64_t need = std::min<uint64_t>(n_slots, slots_per_pass) * per_slot;
     if (need > c.sbuf_paths) {  // grow the ordered sample buffer (first render only)
