@@ -217,14 +217,9 @@ struct alignas(16) DevFar {
   float s0, l, l0;
   uint32_t n_bvh;        // BVH primitives (prims[0 .. n_bvh)): the flat pass of trace_far
   uint32_t nodes_back;   // bytes from the node table to the prim table (both in the scene block)
-  uint32_t pad0;
-  // the far-path queue of this device copy (set by the host when it allocates it): the path ids handed to the far-path
-  // kernel, capacity farq_cap; the count lives in the render counters ([28]; [29] is the far-path kernel's dispenser)
-  uint64_t farq;
-  uint64_t farq_cap;
-  uint64_t pad1;
+  uint32_t pad[2];
 };
-static_assert(sizeof(DevFar) == 112, "DevFar must be 112 B");
+static_assert(sizeof(DevFar) == 96, "DevFar must be 96 B");
 
 constexpr uint32_t DEVFAR_BACK = 256;  // prims - DEVFAR_BACK bytes = the DevFar record
 

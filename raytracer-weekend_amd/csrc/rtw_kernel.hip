@@ -595,8 +595,6 @@ __device__ __forceinline__ void test_sphere32(const DevScene& S, uint32_t pi, fl
 // List-mode kernels (F_LIST): a winner whose t is NaN (an in-plane hit, see rect_list_test) is carried with best
 // t = +inf and this bit in its index (list worlds have few prims); trace_begin hands it on with t = NaN
 constexpr int32_t RECT_NAN_HIT = 0x40000000;
-// Best::prim of a segment a main path kernel hands to the far-path kernel (path_kernel DEFER / FARQ): a miss here
-constexpr int32_t FAR_HANDOFF = -3;
 
 // LOCAL: `wr` already is the prim's object-space ray (the caller caches it per wrapper chain)
 // UNI: pi is wave-uniform (the always list): scalar loads (uload)
@@ -889,12 +887,13 @@ __device__ __forceinline__ void trace_rect_list(const DevScene& S, const Ray& r,
 // inside the r = 1000 ground sphere: ~5% of jumpy-balls' segments) the reference's f32 sphere test "hits" a sphere
 // up to delta(D) outside it (its cancellation grows with D²), and its flat list finds such a hit wherever it lies.
 // trace_begin tests the BVH box grown by delta(D) first -- almost every far ray misses it and skips the BVH -- and
-// the rest (~5e-5 of jumpy-balls' segments) walk the tree here with every box grown by delta(D): a plain stack walk
-// over the global f32 node table (order never changes the answer: closest t, ties to the larger key), the lane's
-// own LDS stack column as its stack (its main walk has not started), each hit leaf's primitives tested in turn.  A
-// push past the column (never for a tree whose stack bound fits it) sends the lane through every BVH primitive.
-// It runs in the far-path kernel (path_kernel FARQ) only: inlined into the main kernels, even never executed, its
-// code cost them 5-9% through register and SGPR pressure (profiles/r06/experiments).
+// the rest (~5e-5 of jumpy-balls' segments) walk the tree here with every box grown by delta(D): a stack walk over
+// the f32 node table (order never changes the answer: closest t, ties to the larger key) that descends into the
+// nearest child hit, the lane's own LDS stack column as its stack (its main walk has not started), each hit leaf's
+// primitives tested in turn.  A push past the column (never for a tree whose stack bound fits it) sends the lane
+// through every BVH primitive.  Inlined into the main kernels, where the segment starts (profiles/r06/experiments:
+// a far-path kernel that replayed the few paths needing it cost the same at 1080p but added its tail, one path's
+// latency, to every frame: configs[0] -30%).
 // The DevFar record, DEVFAR_BACK bytes before the prim table, re-derived at each use (the asm hides the pointer's
 // provenance): otherwise the compiler hoists its ~20 kernel-uniform values into SGPRs held across the whole path
 // loop, which spilled other SGPRs into VGPR lanes (v_readlane / v_writelane in the hot loop: jumpy-1080p -7%)
@@ -994,15 +993,11 @@ constexpr bool far_kernel_feat(uint32_t feat) {
   return !(feat & F_LIST) && (feat & (F_SPHERE | F_MSPHERE | F_MEDIUM)) && feat != F_MESHES;
 }
 // C16: the kernel's LDS stack holds 16-bit entries (the LDS-node and S16 walks), else 32-bit ones (stk); trace_far
-// borrows the lane's column.  Returns true for a lane whose segment needs the far-origin walk.  DEFER (the main path
-// kernels): such a lane does not take the walk here and the path kernel hands the path to the far-path kernel
-// (path_kernel FARQ), so the walk's code is not inlined into the hot kernels (inlined, it cost jumpy-1080p 5-9% by
-// register and SGPR pressure alone, profiles/r06/experiments)
-template <bool COUNT, uint32_t FEAT, int STACK = 1, int BLK = BLOCK, bool C16 = false, bool DEFER = false, int NCAP = 0>
-__device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
+// borrows the lane's column.  A lane whose segment needs the far-origin walk takes it here, instead of the main walk.
+template <bool COUNT, uint32_t FEAT, int STACK = 1, int BLK = BLOCK, bool C16 = false, int NCAP = 0>
+__device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, TraceState& ts, uint32_t* cnt,
                                             uint64_t seg, uint16_t* stk16 = nullptr, int32_t* stk = nullptr,
                                             uint32_t* err = nullptr, const float4* lnodes = nullptr) {
-  bool deferred = false;
   ts.b = Best{INFINITY, 0u, -1, 0.0f, 0.0f};
   // list-mode worlds of rects only (the F_BOXES | F_LIST kernel)
   constexpr bool RECT_LIST = (FEAT & F_LIST) && (FEAT & F_RECT) && !(FEAT & (F_SPHERE | F_MSPHERE | F_TRI | F_MEDIUM));
@@ -1081,12 +1076,9 @@ __device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, Tra
           need = tn <= tf;
         }
         walk = !far;
-        if (DF == 5) asm volatile("" ::"v"((uint32_t)need));  // timing diagnostic: the test kept, no hand-off
-        deferred = need && DF != 3 && DF != 5;
-        if constexpr (!DEFER) {
-          if (__builtin_expect(__any(need), 0))
-            if (need) trace_far<COUNT, FEAT, STACK, BLK, C16, NCAP>(S, r, ts.b, delta, stk16, stk, cnt, seg, err, lnodes);
-        }
+        if (DF == 5) asm volatile("" ::"v"((uint32_t)need));  // timing diagnostic: the test kept, no far walk
+        if (DF != 3 && DF != 5 && __builtin_expect(__any(need), 0))
+          if (need) trace_far<COUNT, FEAT, STACK, BLK, C16, NCAP>(S, r, ts.b, delta, stk16, stk, cnt, seg, err, lnodes);
       }
     }
   }
@@ -1104,7 +1096,6 @@ __device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, Tra
   ts.pend = 0;
   ts.sp = 0;
   ts.on = true;
-  return deferred;
 }
 
 // while-while walk of the 4-wide BVH with postponed leaves (Aila & Laine 2009): phase 1 visits
@@ -1128,9 +1119,6 @@ __device__ __forceinline__ bool trace_begin(const DevScene& S, const Ray& r, Tra
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
 // HN: the walk reads the half-precision node table (DevNode4h: 4 loads / 64 B per visit instead of 7 / 112 B)
-#ifndef RTW_FAR_INLINE
-#define RTW_FAR_INLINE 1  // the far-origin walk inlined into the main kernels; 0 = deferred to the far-path kernel (A/B)
-#endif
 #ifndef RTW_SRING
 #define RTW_SRING 1  // path starts made a ring of 64 at a time (path_kernel SRING; 0 = each lane's own, for A/B)
 #endif
@@ -1780,13 +1768,8 @@ __device__ __forceinline__ bool start_path(const StartArgs& a, uint64_t pid, Pat
 
 // BLK: workgroup size (256, or 512 for the LDS-node variants: one copy of the node table serves 8
 // waves).  NCAP: capacity of the LDS node table in node4s (0 = nodes read from global memory).
-// FARQ: the far-path kernel.  The main kernels (FARQ = false) of worlds with sphere tests in the BVH hand every path
-// whose next segment needs the far-origin walk (trace_begin, trace_far) to a queue (its path id, DevFar::farq) and
-// take a new path; this kernel, launched after each main pass, replays those paths from their start (a path is a
-// function of its id: the same draws, the same hits) and runs them to the end with the walk inlined, counting only
-// the segments after the handed-over one.  Its speed hardly matters (jumpy-1080p: ~0.6 ms of a 110 ms frame).
 template <bool COUNT, int STACK, bool SPILL, int OCC, uint32_t FEAT, int BLK = BLOCK, int NCAP = 0, bool HN = false,
-          bool S16 = false, bool FARQ = false>
+          bool S16 = false>
 __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void path_kernel(RenderArgs a) {
   // + 1: trace_run's branch-free push.  LDS-node variants use 16-bit entries, STACK rows (window included);
   // S16 (global nodes, 16-bit entries): STACK + 1 rows of 16 bits
@@ -1840,26 +1823,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   };
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
-  // the far-path queue's count and this kernel's dispenser (counters [28], [29]), derived from the path queue's
-  // address where used (kernel arguments read in the loop are hoisted into SGPRs held across it)
-  auto farq_word = [&](int k) {
-    unsigned long long* q = a.queue;
-    asm volatile("" : "+s"(q));
-    return q - 3 + k;
-  };
-  constexpr bool DEFER = !FARQ && far_kernel_feat(FEAT) && !RTW_FAR_INLINE;
-  const uint64_t P = FARQ ? *(volatile unsigned long long*)farq_word(0) : a.n_paths;
-  unsigned long long* const dispenser = FARQ ? farq_word(1) : a.queue;
-  // ids per dispenser atomic: the far-path kernel sizes it from the queued count (a.batch = 64 for the usual few
-  // thousand; ~32 batches per wave when a far camera hands over most of a frame's paths)
-  const uint32_t batch = FARQ ? (uint32_t)min(max(P / ((uint64_t)gridDim.x * (BLK / 64) * 32u), (uint64_t)a.batch), (uint64_t)1024)
-                              : a.batch;
-  // the far-path kernel's grid is the resident one, but its queue is usually a few thousand paths: the waves beyond
-  // the batches there are leave at once instead of each taking (and losing) a turn at the dispenser's atomic
-  if (FARQ && (uint64_t)(blockIdx.x * (BLK / 64) + (threadIdx.x >> 6)) * batch >= P) return;
-  // FARQ: the lane replays a handed-over path; its segments up to and including the one that needs the far walk (the
-  // first such) were counted by the main kernel
-  bool replay = false;
+  const uint64_t P = a.n_paths;
+  unsigned long long* const dispenser = a.queue;
+  const uint32_t batch = a.batch;
   uint32_t cnt[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
@@ -1876,7 +1842,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   // Per lane slot: o, d, time, rng (2 words), pid (10 words, structure of arrays); rng = 0 marks an off-image id.
   // (the rect list kernel only: its LDS is free and its VGPRs hold the generation; the LDS-node and mesh kernels have
   // no LDS left for 2.5 KB per wave at their occupancy)
-  constexpr bool SRING = RTW_SRING && FEAT == (F_BOXES | F_LIST) && !FARQ && !LST;
+  constexpr bool SRING = RTW_SRING && FEAT == (F_BOXES | F_LIST) && !LST;
   __shared__ uint32_t ring_lds[SRING ? (BLK / 64) * 640 : 1];
   __shared__ uint32_t ring_head_lds[SRING ? BLK / 64 : 1];
   uint32_t* const ring = ring_lds + (SRING ? (threadIdx.x >> 6) * 640u : 0u);
@@ -1986,15 +1952,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
       if (!has) {
         const uint64_t id = rank < avail ? pool_next + rank : nb + (rank - avail);
-        if constexpr (FARQ) {  // replay a handed-over path from its start (its id in the queue)
-          if (rank < avail || id < ne) {
-            const uint32_t pid = reinterpret_cast<const uint32_t*>(far_record(S)->farq)[id];
-            if (start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, pid, st, stk16)) {
-              has = true;
-              replay = true;
-            }
-          }
-        } else if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, id, st, stk16)) {
+        if ((rank < avail || id < ne) && start_path<SLDS, LST ? BLK : 0, LST_ROW0, AB>(SA, id, st, stk16)) {
           has = true;
         }
       }
@@ -2015,17 +1973,12 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     phase(0);
     // segments starting now, counted per wave with every lane active (so the count is uniform
     // and stays in SGPRs)
-    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on && !replay));
+    nrays += (unsigned long long)__popcll(__ballot(has && !ts.on));
     if (!has) continue;
     // ---- one segment: closest hit (resumable) + shading (lib.rs:97-117)
     if (!ts.on) {
-      const bool far = trace_begin<COUNT, FEAT, STACK, BLK, (NCAP > 0 || S16), DEFER, (HN ? 0 : NCAP)>(
-          S, st.ray, ts, cnt, st.rng, stk16, stk, a.err, nodes_lds);
-      // DEFER: the segment needs the far-origin walk: it ends as a "miss" here (the hit record's prim FAR_HANDOFF, no
-      // walk) and the miss branch hands the path to the far-path kernel, whose replay overwrites its sample.  (Leaving
-      // the loop body early instead -- a `continue` -- cost the hot loop 5% through the control-flow structurizer.)
-      if constexpr (DEFER) ts.b.prim = far ? FAR_HANDOFF : ts.b.prim;
-      if constexpr (FARQ) replay = replay && !far;  // from the next segment on, the replay's segments count
+      trace_begin<COUNT, FEAT, STACK, BLK, (NCAP > 0 || S16), (HN ? 0 : NCAP)>(S, st.ray, ts, cnt, st.rng, stk16, stk,
+                                                                              a.err, nodes_lds);
     }
     if (!(FEAT & F_LIST)) {
       const uint32_t act = (uint32_t)__popcll(__ballot(1));
@@ -2061,20 +2014,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     if (b.prim < 0) {  // lib.rs:102-105
       L = mul(path_T(), bg);
       done = true;
-      if constexpr (DEFER) {
-        if (__builtin_expect(b.prim == FAR_HANDOFF, 0)) {  // hand the path (its id) to the far-path kernel
-          // one atomic per wave (the handing-over lanes' count; the host sizes the queue for every path): per lane,
-          // a frame whose camera is far from the BVH (every path handed over) queued on the one counter word
-          const uint64_t m = __ballot(1);
-          const int lead = __builtin_ctzll(m);
-          unsigned long long base = 0;
-          if ((int)lane == lead) base = atomicAdd(farq_word(0), (unsigned long long)__popcll(m));
-          base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), lead) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, lead);
-          const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          reinterpret_cast<uint32_t*>(far_record(S)->farq)[base + rk] = LST ? lst_ld(4) : st.pid;
-        }
-      }
       if (__builtin_expect(b.prim == -2, 0)) {
         // trace_run tripped its guard (a corrupt tree; the frame is invalid and reported): close the path queue
         // for every wave and empty this wave's id pool, so the grid drains after about one trip per wave
@@ -2438,7 +2377,6 @@ int upload(Scene& s, int device) {
     c.scene.nodes = (const DevNode4*)(base + o_nodes);
     c.scene.hnodes = f.nodes4h.empty() ? nullptr : (const DevNode4h*)(base + o_hnodes);
     c.scene.prims = (const DevPrim*)(base + o_prims);
-    c.far_dev = base + o_far;
     c.scene.always = (const uint32_t*)(base + o_always);
     c.scene.tshade = (const DevTriShade*)(base + o_tsh);
     c.scene.insts = (const DevInst*)(base + o_inst);
@@ -2480,7 +2418,7 @@ void release(Scene& s) {
     if (c.err_host) hipHostFree(c.err_host);
     if (c.sbuf) hipFree(c.sbuf);
     if (c.spill) hipFree(c.spill);
-    for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids, &c.farq}) free_buf(*b);
+    for (DevBuf* b : {&c.image, &c.tiles, &c.packed, &c.gathered, &c.gather_ids}) free_buf(*b);
     for (void* e : c.ev)
       if (e) hipEventDestroy(static_cast<hipEvent_t>(e));
     for (void* e : c.gev)
@@ -2613,18 +2551,6 @@ static Variant pick_kernel(uint32_t feat, uint32_t need, bool list, uint32_t n_n
       return pick5<C, F_ALL>(need);
   }
 }
-// the far-path kernel (path_kernel FARQ), run after each main pass of a world whose BVH holds sphere tests
-// (DevScene::far_check): the main kernel's own LDS-node form for the default sphere kernel (a handed-over path replays
-// up to 50 segments one after another, so the far pass lasts about one path's latency: 2.1 ms per jumpy-1080p frame
-// with the generic kernel's global node reads, r06), else the generic all-features walk with the HBM stack spill
-static Variant far_kernel_variant(bool count, const Variant& main) {
-  using namespace dev;
-  if (main.k16 && main.block == 1024u && main.stack == 16u)
-    return count ? Variant{path_kernel<true, 16, false, 8, F_SPHERES, 1024, 144, false, false, true>, 16u, 1024u, true}
-                 : Variant{path_kernel<false, 16, false, 8, F_SPHERES, 1024, 144, false, false, true>, 16u, 1024u, true};
-  return count ? Variant{path_kernel<true, STACK_DEEP5, true, 5, F_ALL, BLOCK, 0, false, false, true>, (uint32_t)STACK_DEEP5}
-               : Variant{path_kernel<false, STACK_DEEP5, true, 5, F_ALL, BLOCK, 0, false, false, true>, (uint32_t)STACK_DEEP5};
-}
 static Variant path_kernel_variant(bool count, const Flat& f) {
   const uint32_t feat = f.features, need = f.stack_need, need4 = f.stack_need4, nn = (uint32_t)f.nodes4.size();
   const bool list = f.nodes4.empty();
@@ -2633,9 +2559,9 @@ static Variant path_kernel_variant(bool count, const Flat& f) {
                : pick_kernel<false>(feat, need, list, nn, need4, f.codes16, hh, f.far_check != 0);
 }
 
-static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count, bool farq = false) {
-  int& g = c.grid[(count ? 1 : 0) + (farq ? 2 : 0)];
-  void*& gf = c.grid_fn[(count ? 1 : 0) + (farq ? 2 : 0)];
+static int resident_grid(DeviceCopy& c, path_fn fn, uint32_t block, bool count) {
+  int& g = c.grid[count ? 1 : 0];
+  void*& gf = c.grid_fn[count ? 1 : 0];
   if (g > 0 && gf == (void*)fn) return g;
   gf = (void*)fn;
   int per_cu = 0, cus = 0;
@@ -2735,7 +2661,6 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
     HIPCHK(hipMemsetAsync(d_out, 0, n * sizeof(float), stream), "hipMemsetAsync(out)");
   } else if (n_slots) {
     const uint64_t per_slot = 64ull * spp;
-    const bool farq = sc.flat.far_check != 0 && !RTW_FAR_INLINE;
     const uint32_t slots_per_pass = (uint32_t)std::max<uint64_t>(1, max_pass_paths() / per_slot);
     const uint64_t need = std::min<uint64_t>(n_slots, slots_per_pass) * per_slot;
     if (need > c.sbuf_paths) {  // grow the ordered sample buffer (first render only)
@@ -2792,36 +2717,6 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       c.spill_bytes = spill_bytes;
     }
     a.spill = c.spill;
-    // the far-path kernel: its own grid and spill rows (it shares the spill area: it runs after the main pass), and the
-    // queue, room for every path id of a pass (4 B each: 4.2 GB at jumpy-1080p x 512), whose address the device's
-    // DevFar record holds
-    RenderArgs af = a;
-    Variant fvar{};
-    int fgrid = 0;
-    if (farq) {
-      fvar = far_kernel_variant(count, var);
-      fgrid = resident_grid(c, fvar.fn, fvar.block, count, true);
-      af.spill_depth = (!fvar.k16 && sc.flat.stack_need > fvar.stack) ? sc.flat.stack_need - fvar.stack : 0;
-      af.spill_lanes = (uint32_t)fgrid * fvar.block;
-      af.batch = 64;
-      const size_t fbytes = (size_t)af.spill_depth * af.spill_lanes * sizeof(int32_t);
-      if (fbytes > c.spill_bytes) {
-        if (c.spill) HIPCHK(hipFree(c.spill), "hipFree(stack spill)");
-        c.spill = nullptr;
-        c.spill_bytes = 0;
-        HIPCHK(hipMalloc((void**)&c.spill, fbytes), "hipMalloc(stack spill)");
-        c.spill_bytes = fbytes;
-      }
-      a.spill = af.spill = c.spill;
-      const uint64_t cap = need;  // paths of the largest pass
-      if (cap * sizeof(uint32_t) > c.farq.cap) {
-        HIPCHK(hipStreamSynchronize(stream), "hipStreamSynchronize");  // an earlier render may still read the queue
-        if (int e = grow(c.farq, cap * sizeof(uint32_t))) return e;
-        const uint64_t rec[2] = {(uint64_t)(uintptr_t)c.farq.p, cap};
-        HIPCHK(hipMemcpy(static_cast<char*>(c.far_dev) + offsetof(DevFar, farq), rec, sizeof rec, hipMemcpyHostToDevice),
-               "hipMemcpy(far queue)");
-      }
-    }
     for (uint32_t base = 0; base < n_slots; base += slots_per_pass) {
       const uint32_t ns = std::min(slots_per_pass, n_slots - base);
       a.slot_base = base;
@@ -2829,20 +2724,13 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       a.batch = batch0;
       if (batch_auto)
         while (a.batch / 2u >= batch_floor && a.n_paths < (uint64_t)a.batch * waves * 32u) a.batch /= 2u;
-      // the far-path queue's count and dispenser ([28], [29]) and the path queue ([31])
-      if (base) HIPCHK(hipMemsetAsync(a.queue - 3, 0, 4 * sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
+      if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
       hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");
       HIPCHK(hipEventRecord(ke[0], stream), "hipEventRecord");
       hipLaunchKernelGGL(fn, dim3(grid), dim3(var.block), 0, stream, a);
       HIPCHK(hipGetLastError(), "path_kernel launch");
-      if (farq) {  // the paths the pass handed over (DevFar::farq), to the end; timed with the pass
-        af.slot_base = a.slot_base;
-        af.n_paths = a.n_paths;
-        hipLaunchKernelGGL(fvar.fn, dim3(fgrid), dim3(fvar.block), 0, stream, af);
-        HIPCHK(hipGetLastError(), "far-path kernel launch");
-      }
       HIPCHK(hipEventRecord(ke[1], stream), "hipEventRecord");
       c.kev_head = (c.kev_head + 1) % 64u;
       c.kev_count = std::min(c.kev_count + 1u, 64u);

@@ -108,10 +108,8 @@ struct DeviceCopy {
   void* kev[64][2] = {};                   // hipEvent_t pairs around path-kernel launches (ring,
                                            // rtw_path_kernel_times)
   uint32_t kev_head = 0, kev_count = 0;
-  int grid[4] = {0, 0, 0, 0};              // resident path_kernel grid (plain, counting; the far-path kernel's at
-  void* grid_fn[4] = {};                   // [2], [3]) of the variant it was computed for (knobs may switch variants)
-  DevBuf farq;                             // the far-path queue (path ids; DevFar::farq points here)
-  void* far_dev = nullptr;                 // the scene block's DevFar record on this device
+  int grid[2] = {0, 0};                    // resident path_kernel grid (plain, counting) of the
+  void* grid_fn[2] = {nullptr, nullptr};   // variant it was computed for (knobs may switch variants)
   // device buffers kept across render calls (grown, never shrunk; freed by release()): a
   // 30-camera animation through rtw_render does no hipMalloc after the first frame
   DevBuf image, tiles, packed, gathered, gather_ids;

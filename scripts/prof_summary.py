@@ -36,7 +36,7 @@ for k, v in out["pmc"].items():
     v["fetch_bytes_per_launch_raw"] = fetch
     v["write_bytes_per_launch"] = write
     v["hbm_bytes_per_launch"] = 2 * fetch + write
-main = [k for k in out["pmc"] if "path_kernel<false" in k and not k.endswith(", true>(rtw::RenderArgs)")]
+main = [k for k in out["pmc"] if "path_kernel<false" in k]
 if main:
     out["hbm_bytes_per_launch"] = out["pmc"][main[0]]["hbm_bytes_per_launch"]
     out["kernel"] = main[0]

@@ -30,20 +30,10 @@ import bench  # noqa: E402  (flop model and peaks; bench imports torch only insi
 
 
 def rocprof_avg_ms(path: Path) -> float:
-    """The main path kernel's average duration, plus the far-path kernel's time per main launch where the
-    world has one (round 6: `path_kernel<..., true>`, launched after each main launch and inside the HIP
-    events bench.py times)."""
-    main = far = None
     for r in csv.DictReader(open(path)):
-        if "path_kernel<false" not in r["Name"]:
-            continue
-        if r["Name"].endswith(", true>(rtw::RenderArgs)"):
-            far = far or (float(r["TotalDurationNs"]), int(r["Calls"]))
-        else:
-            main = main or (float(r["TotalDurationNs"]), int(r["Calls"]))
-    if main is None:
-        raise SystemExit(f"no path_kernel<false,...> row in {path}")
-    return (main[0] + (far[0] if far else 0.0)) / main[1] / 1e6
+        if "path_kernel<false" in r["Name"]:
+            return float(r["AverageNs"]) / 1e6
+    raise SystemExit(f"no path_kernel<false,...> row in {path}")
 
 
 def main():

@@ -20,13 +20,11 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def per_dispatch(path, name_key="Kernel_Name", match="path_kernel<false"):
-    """Counters per dispatch of the main path kernel, averaged.  The far-path kernel (round 6: the same
-    template with its last argument, FARQ, true; launched after the main one on sphere-BVH worlds) matches the
-    same prefix and is left out."""
+    """Counters per dispatch of the path kernel, averaged."""
     per = defaultdict(lambda: defaultdict(float))
     kernel = None
     for r in csv.DictReader(open(path)):
-        if match not in r[name_key] or r[name_key].endswith(", true>(rtw::RenderArgs)"):
+        if match not in r[name_key]:
             continue
         d = r.get("Dispatch_Id") or r.get("Correlation_Id") or "0"
         per[d][r["Counter_Name"]] += float(r["Counter_Value"])

@@ -24,8 +24,8 @@ def load(path):
     per = defaultdict(lambda: defaultdict(float))  # dispatch -> counter -> value
     kernel = None
     for r in csv.DictReader(open(path)):
-        if "path_kernel<false" not in r["Kernel_Name"] or r["Kernel_Name"].endswith(", true>(rtw::RenderArgs)"):
-            continue  # (the far-path kernel, round 6, is not the main kernel)
+        if "path_kernel<false" not in r["Kernel_Name"]:
+            continue
         d = r.get("Dispatch_Id") or r.get("Correlation_Id") or "0"
         per[d][r["Counter_Name"]] += float(r["Counter_Value"])
         kernel = r["Kernel_Name"]
