@@ -1119,6 +1119,9 @@ __device__ __forceinline__ void trace_begin(const DevScene& S, const Ray& r, Tra
 // Which nodes are visited in which order never changes the answer (closest hit, ties to the
 // larger key, over every leaf not culled).
 // HN: the walk reads the half-precision node table (DevNode4h: 4 loads / 64 B per visit instead of 7 / 112 B)
+#ifndef RTW_MESH_ROOT
+#define RTW_MESH_ROOT 5  // node4s of the S16 mesh walk's LDS copy of the tree top (trace_run ROOT; 0 = none, 1 = root)
+#endif
 #ifndef RTW_SRING
 #define RTW_SRING 1  // path starts made a ring of 64 at a time (path_kernel SRING; 0 = each lane's own, for A/B)
 #endif
@@ -1174,6 +1177,72 @@ __device__ void trace_run(const DevScene& S, const Ray& r, TraceState& ts, int32
   const uint32_t fx = nx ^ 16u, fy = ny ^ 16u, fz = nz ^ 16u;
   const char* const NB = NCAP > 0 ? reinterpret_cast<const char*>(lnodes)
                                   : (HN ? reinterpret_cast<const char*>(S.hnodes) : reinterpret_cast<const char*>(S.nodes));
+  // ROOT (the S16 half-node mesh walk): lanes at the root or one of its children (breadth-first ids 0..4) visit it
+  // from the workgroup's LDS copy of those five node4s (lnodes) before the loop, twice, so a segment's first two
+  // visits cost no vector-memory loads (the mesh kernels are bound on the vector-memory data path, TD: ~2 of
+  // monument's 5.6 visits per ray).  monument-4k +0.7%, cow-1080p +0.5-0.7% (profiles/r06/experiments rt5); the
+  // same in the loop itself (t1: the tree's top from LDS at every visit) lost 6%: a visit whose lanes straddle the
+  // table's edge runs both load paths, and the branch breaks up the loop's load clause.  17 node4s, three levels: -3.6%.
+  constexpr bool ROOT = HN && S16 && NCAP == 0 && RTW_MESH_ROOT > 0;
+  constexpr int32_t NROOT = RTW_MESH_ROOT;  // node4s in the LDS copy: 1 = the root, 5 = the root and its children
+#pragma unroll
+  for (int lv = 0; lv < (ROOT ? (NROOT > 1 ? 2 : 1) : 0); ++lv) {
+    if (__any(ts.node >= 0 && ts.node < NROOT)) {
+      if (ts.node >= 0 && ts.node < NROOT) {
+        const char* const TB = reinterpret_cast<const char*>(lnodes) + (uint32_t)ts.node * 112u;
+        const uint4 px = *reinterpret_cast<const uint4*>(TB + nx);
+        const uint4 py = *reinterpret_cast<const uint4*>(TB + ny);
+        const uint4 pz = *reinterpret_cast<const uint4*>(TB + nz);
+        const uint4 cq = *reinterpret_cast<const uint4*>(TB + 96u);
+        const half2_t oxy = as_h2(cq.z), oz = as_h2(cq.w);
+        const V3 bs = mk(__builtin_fmaf((float)oxy.x, inv.x, -ood.x), __builtin_fmaf((float)oxy.y, inv.y, -ood.y),
+                         __builtin_fmaf((float)oz.x, inv.z, -ood.z));
+        const uint32_t PQ[3][4] = {{px.x, px.y, px.z, px.w}, {py.x, py.y, py.z, py.w}, {pz.x, pz.y, pz.z, pz.w}};
+        float NA[3][4], FA[3][4];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const half2_t n01 = as_h2(PQ[q][0]), n23 = as_h2(PQ[q][1]), f01 = as_h2(PQ[q][2]), f23 = as_h2(PQ[q][3]);
+          NA[q][0] = (float)n01.x; NA[q][1] = (float)n01.y; NA[q][2] = (float)n23.x; NA[q][3] = (float)n23.y;
+          FA[q][0] = (float)f01.x; FA[q][1] = (float)f01.y; FA[q][2] = (float)f23.x; FA[q][3] = (float)f23.y;
+        }
+        const int32_t CW[4] = {(int32_t)(int16_t)(cq.x & 0xFFFFu), (int32_t)cq.x >> 16, (int32_t)(int16_t)(cq.y & 0xFFFFu),
+                               (int32_t)cq.y >> 16};
+        if (COUNT) {
+          cnt[0]++;
+          cnt[14] += (CW[0] != 0) + (CW[1] != 0) + (CW[2] != 0) + (CW[3] != 0);
+        }
+        const float tmax_c = __builtin_fmaf(ts.b.t, 1.0e-5f, ts.b.t) + 1.0e-5f;
+        int32_t next = -1, bk = -1;
+        float best = INFINITY;
+        bool hit[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // conservative slab test (culling only), as in the loop below
+          const float a0 = __builtin_fmaf(NA[0][k], inv.x, bs.x), b0 = __builtin_fmaf(NA[1][k], inv.y, bs.y);
+          const float c0 = __builtin_fmaf(NA[2][k], inv.z, bs.z);
+          const float d0 = __builtin_fmaf(FA[0][k], inv.x, bs.x), e0 = __builtin_fmaf(FA[1][k], inv.y, bs.y);
+          const float f0 = __builtin_fmaf(FA[2][k], inv.z, bs.z);
+          const float tn = fmaxf(fmaxf(fmaxf(a0, b0), c0), 0.0f);
+          hit[k] = tn <= fminf(fminf(fminf(d0, e0), f0), tmax_c);
+          const bool in = hit[k] & (CW[k] >= 0) & (tn < best);
+          best = in ? tn : best;
+          bk = in ? k : bk;
+          next = in ? CW[k] : next;
+        }
+        int32_t pend = ts.pend, sp = ts.sp;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool leaf_take = hit[k] & (CW[k] < 0) & (pend == 0);
+          pend = leaf_take ? CW[k] : pend;
+          const bool pk = hit[k] & (k != bk) & !leaf_take;
+          stk16[sp * BLK] = (uint16_t)CW[k];
+          sp += pk ? 1 : 0;
+        }
+        ts.pend = pend;
+        ts.sp = sp;
+        ts.node = next;
+      }
+    }
+  }
   // every wave must drain: a corrupt tree (a cycle) ends the walk instead of hanging the GPU, and
   // sets the device's host-mapped error word (RenderArgs::err), which the host turns into RTW_EINVAL
   // at the next render call, rtw_render_status, rtw_path_kernel_times or a stats read
@@ -1780,10 +1849,16 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   constexpr int LST_ROW0 = STACK + (S16 ? 1 : 0);
   __shared__ uint16_t stk16_all[NCAP > 0 ? (STACK + LST_ROWS) * BLK : (S16 ? (STACK + 1 + LST_ROWS) * BLK : 1)];
   constexpr uint32_t NODE_Q = HN ? 7u : 8u;  // 16-B quads per node (DevNode4h / DevNode4)
-  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : 1];
+  // (the S16 half-node mesh walk: the root node only, trace_run ROOT)
+  constexpr bool ROOT_LDS = HN && S16 && NCAP == 0 && RTW_MESH_ROOT > 0;
+  __shared__ float4 nodes_lds[NCAP > 0 ? NCAP * NODE_Q : (ROOT_LDS ? RTW_MESH_ROOT * NODE_Q : 1)];
   if constexpr (NCAP > 0) {  // the host launches this variant only when Flat::codes16 and n_nodes <= NCAP
     const float4* g = HN ? reinterpret_cast<const float4*>(a.scene.hnodes) : reinterpret_cast<const float4*>(a.scene.nodes);
     for (uint32_t k = threadIdx.x; k < a.scene.n_nodes * NODE_Q; k += BLK) nodes_lds[k] = g[k];
+  }
+  if constexpr (ROOT_LDS) {
+    const uint32_t nq = min(a.scene.n_nodes, (uint32_t)RTW_MESH_ROOT) * NODE_Q;
+    if (threadIdx.x < nq) nodes_lds[threadIdx.x] = reinterpret_cast<const float4*>(a.scene.hnodes)[threadIdx.x];
   }
   // start_path's operands from LDS in the sphere and list-mode variants (their SGPR spills, and every
   // reload a v_readlane: cornell-800 +6%, jumpy +0.8%) and in the 6 / 7-wave mesh walk (S16): at 80 VGPRs its

@@ -182,6 +182,38 @@ def test_pass_with_path_ids_above_2_31(gpu, knobs):
     assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
 
 
+def test_start_ring_passes_and_tiles(gpu, knobs):
+    """The rect list kernel's path starts come from a per-wave ring of 64 made at once from consecutive ids of the
+    wave's pool.  A frame split into passes (the pool restarts at each) and packed tile
+    renders of a ragged frame (off-image ids inside the ring) must give the one-pass full frame's bits and rays."""
+    torch = pytest.importorskip("torch")
+    rtw = gpu
+    s = rtw.Scene()
+    cam, bg = s.preset("cornell-box", 1.0, seed=3)
+    s.commit(device=0)
+    w, h, spp = 96, 96, 2048  # 18.9 M paths: two passes of 2^24
+    one, st1 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=11).render()
+    knobs.setenv("RTW_PASS_LOG2", "24")
+    split, st2 = rtw.Raytracer(s, cam, bg, w, h, spp, seed=11).render()
+    assert st1["rays"] == st2["rays"]
+    assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
+    w, h, spp = 44, 21, 3  # ragged: 6 x 3 tiles, the last column and row partly outside
+    rt = rtw.Raytracer(s, cam, bg, w, h, spp, seed=5)
+    full, _ = rt.render()
+    nt = rtw.n_tiles(w, h)
+    img = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
+    for world in (1, 2, 5):
+        for rank in range(world):
+            ids = torch.arange(rank, nt, world, dtype=torch.int32, device="cuda:0")
+            packed = torch.zeros((len(ids), 64, 3), dtype=torch.float32, device="cuda:0")
+            rt.render_device(packed.data_ptr(), 0, ids.data_ptr(), len(ids),
+                             torch.cuda.current_stream().cuda_stream)
+            rtw.unpack_tiles_device(w, h, ids.data_ptr(), len(ids), packed.data_ptr(), img.data_ptr(), 0,
+                                    torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(img.cpu().numpy().view(np.uint32), full.view(np.uint32)), world
+
+
 def test_path_kernel_times(gpu):
     rtw = gpu
     s = rtw.Scene()
