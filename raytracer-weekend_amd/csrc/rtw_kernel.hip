@@ -759,9 +759,9 @@ __device__ __forceinline__ void rect_list_test(const Ray& lr, V3 y, float4 q0, f
     const float t = div_by_recip(num, d_k, y_k);
     const float x = o_a + t * d_a;
     const float yy = o_b + t * d_b;
-    // the three tests as one: each med3 equals its value exactly when in range, so the largest |med3 - value| is 0
-    // exactly when all three pass (t, x, y are finite here).  One compare and no scalar ands: the scalar unit, which
-    // a CU's four SIMDs share, bounds this loop (2 more VALU, 2 fewer SALU per rect: cornell-800 +1.5%, r05z)
+    // the three tests as one: each med3 equals its value exactly when in range, so the largest |med3 - value| is 0 exactly
+    // when all pass (t finite; x, y finite or +-inf, and +-inf lies outside the rect's finite bounds, rect_fast: inf, a
+    // rejection as the reference's).  One compare, no scalar ands (+2 VALU, -2 SALU per rect: cornell-800 +1.5%, r05z)
     const float m1 = __builtin_amdgcn_fmed3f(t, TMIN, bt), m2 = __builtin_amdgcn_fmed3f(x, q0.x, q0.y);
     const float m3 = __builtin_amdgcn_fmed3f(yy, q0.z, q0.w);
     acc = fmaxf(fmaxf(fabsf(m1 - t), fabsf(m2 - x)), fabsf(m3 - yy)) == 0.0f;

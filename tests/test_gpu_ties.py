@@ -171,6 +171,31 @@ def test_degenerate_primitives(gpu, orc):
     assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
 
 
+def test_infinite_rect_bounds_list_mode(gpu, orc):
+    """Rects with infinite bounds: an endless floor, a wall unbounded on one side, a ceiling strip.  Their
+    hit points can overflow to +-inf, so the flattener leaves such a world off the rect loop's fast path (rect_fast 0,
+    rtw_scene_info 13) and the IEEE path decides `x < a0 || x > a1` as rectangular.rs:40 does; grazing rays along the
+    floor (the camera a hair above it) included."""
+    rtw = gpu
+    inf = float("inf")
+    s = rtw.Scene()
+    a, b = _mats(s)
+    s.xz_rect(-inf, inf, -inf, inf, 0.0, s.lambertian_solid((0.5, 0.5, 0.5)))  # floor
+    s.xy_rect(-inf, 3.0, 0.0, 4.0, -6.0, a)                                    # wall, unbounded to -x
+    s.yz_rect(0.5, 2.5, -inf, inf, 4.0, b)                                     # strip, unbounded in z
+    s.xz_rect(-1.0, 1.0, -1.0, 1.0, 5.0, s.diffuse_light(s.solid_rgb(4, 4, 4)))
+    cam = rtw.Camera.new((0.0, 1e-3, 6.0), (0.0, 0.5, 0.0), (0, 1, 0), 70.0, W / H, 0.0, 6.0)
+    bg = (0.6, 0.7, 0.9)
+    text, imgs = s.dump(), s.images()
+    s.commit()
+    assert s.info(3) == 0 and s.info(13) == 0  # list mode, off the fast path
+    g, st = rtw.Raytracer(s, cam, bg, W, H, 4, seed=3).render()
+    r, rays = orc.OracleScene(text, imgs).render(orc.camera_from_fields(cam.as_dict()), bg, W, H, 4, seed=3)
+    assert st["rays"] == rays
+    bad = np.argwhere(g.view(np.uint32) != r.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} mismatching components, first {bad[:4].tolist()}"
+
+
 @pytest.mark.parametrize("kernel", ["rect_list", "all_features_list", "generic"])
 @pytest.mark.parametrize("tile,spp", [(2149, 20), (2347, 16)])
 def test_in_plane_bounce_list_mode(gpu, orc, knobs, kernel, tile, spp):
