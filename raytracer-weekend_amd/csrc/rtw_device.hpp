@@ -223,6 +223,12 @@ static_assert(sizeof(DevFar) == 96, "DevFar must be 96 B");
 
 constexpr uint32_t DEVFAR_BACK = 256;  // prims - DEVFAR_BACK bytes = the DevFar record
 
+// The render counters (DeviceCopy::counters): [0, 32) statistics, then DISP path-id dispensers DISP_STRIDE words
+// (128 B) apart (RenderArgs::queue, path_kernel)
+constexpr uint32_t DISP = 8;
+constexpr uint32_t DISP_STRIDE = 16;
+constexpr uint32_t COUNTER_WORDS = 32 + DISP * DISP_STRIDE;
+
 struct DevCamera {
   float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
   float lens_radius, time0, time1;
@@ -252,7 +258,7 @@ struct RenderArgs {
   float* sbuf;                // ordered sample buffer: n_paths x (r, g, b) floats, path-major
   float* out;
   unsigned long long* counters;  // [0] rays, [1] node visits, [2] prim tests, [3..8] per type
-  unsigned long long* queue;     // path-id dispenser of this pass
+  unsigned long long* queue;     // the pass's DISP path-id dispensers (DISP_STRIDE words apart)
   uint32_t* err;                 // host-mapped sticky error word: 1 = a traversal guard tripped (DeviceCopy::err_host)
   int32_t* spill;                // traversal stack entries beyond the LDS stack: [depth][lane]
   uint32_t spill_depth;          // entries per lane (0 = the LDS stack covers the tree's bound)

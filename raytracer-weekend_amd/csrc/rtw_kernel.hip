@@ -1899,18 +1899,50 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   const DevScene& S = a.scene;
   const V3 bg = ld3(a.bg);
   const uint64_t P = a.n_paths;
+  // SHARD (the LDS-node sphere kernels): n dispensers (DISP when the host's small-frame rule cut the batch below these
+  // kernels' 1024, else 1), 128 B apart: dispenser d hands out the
+  // pass's batches d, d + n, d + 2n, ... (interleaved, so the grid still works through the frame in id order, tile
+  // after tile), and a wave takes batches from dispenser (its workgroup + k) mod n, k = 0, 1, ... as each runs dry
+  // (workgroups are dealt to the XCDs in turn, so each XCD's waves start on their own word).  One word for the whole
+  // grid serialises its atomics: the small batches of small passes -- configs[0], an 8-GPU share's short end-of-pass
+  // tail -- queued behind it (r06, share8: jumpy's 1/8 share +5%, configs[0] +11%).  The other kernels keep the one
+  // word (their code with the dispenser loop ran 1.2-1.8% slower on full frames: cornell, monument).
+  constexpr bool SHARD = NCAP > 0;
   unsigned long long* const dispenser = a.queue;
-  const uint32_t batch = a.batch;
+  const uint32_t batch = a.batch, ndisp = batch < 1024u ? DISP : 1u;
+  const uint64_t NB = (P + batch - 1u) / batch;  // batches in the pass
   uint32_t cnt[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long nrays = 0;
   // the wave's id pool [next, end) lives in LDS between regenerations: loop-carried 64-bit
   // uniforms otherwise end up as VGPR phis that the 6-wave sphere variant has to spill
-  __shared__ uint64_t pool_lds[BLK / 64][3];
+  __shared__ uint64_t pool_lds[BLK / 64][SHARD ? 5 : 3];
   // S16 mesh walk: the wave index as a scalar, so the pool address is rebuilt from an SGPR (one v_mov) where it is
   // used instead of kept in a VGPR (the 7-wave walk spilled it to scratch and reloaded it at every regeneration;
   // the sphere and list-mode kernels measured 0.5-1.4% slower with it, profiles/r05/experiments s1)
   uint64_t* const pool = pool_lds[S16 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6];
   if (lane == 0) { pool[0] = 0; pool[1] = 0; }
+  if (SHARD && lane == 0) pool[SHARD ? 4 : 0] = 0;
+  // the wave's next batch [b, e) of path ids (b = e = P: none left); lane 0 takes it, every lane reads it
+  auto refill = [&](uint64_t& b, uint64_t& e) {  // (SHARD)
+    if (lane == 0) {
+      uint64_t bb = P, ee = P;
+      uint32_t k = (uint32_t)pool[4];
+      for (; k < ndisp; ++k) {
+        const uint32_t d = (blockIdx.x + k) & (ndisp - 1u);
+        const uint64_t g = atomicAdd(dispenser + d * DISP_STRIDE, 1ull) * ndisp + d;  // the pass's batch g
+        if (g < NB) {
+          bb = g * batch;
+          ee = bb + batch < P ? bb + batch : P;
+          break;
+        }
+      }
+      pool[2] = bb;
+      pool[SHARD ? 3 : 0] = ee;
+      pool[SHARD ? 4 : 0] = k;
+    }
+    b = rfl64(pool[2]);
+    e = rfl64(pool[SHARD ? 3 : 0]);
+  };
   // SRING: the wave's ring of 64 path starts, made by all 64 lanes at once from 64 consecutive ids of its pool and
   // taken by the lanes that regenerate (start_path is a function of the id alone, so which lane makes a path's start
   // changes nothing).  start_path at full lane occupancy instead of the few idle lanes of each regeneration.
@@ -1972,10 +2004,14 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         if (n_need > have) {  // the ring is spent: 64 more starts from the pool (refilled by one atomic per batch)
           uint64_t pool_next = rfl64(pool[0]), pool_end = rfl64(pool[1]);
           if (pool_next >= pool_end) {
-            if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
-            const uint64_t b = rfl64(pool[2]);
-            pool_next = b < P ? b : P;
-            pool_end = b < P ? (b + batch < P ? b + batch : P) : P;
+            if constexpr (SHARD) {
+              refill(pool_next, pool_end);
+            } else {
+              if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
+              const uint64_t b = rfl64(pool[2]);
+              pool_next = b < P ? b : P;
+              pool_end = b < P ? (b + batch < P ? b + batch : P) : P;
+            }
           }
           if (pool_next < pool_end) {  // pools and passes hold whole multiples of 64 ids
             const uint64_t id = pool_next + lane;
@@ -2013,15 +2049,26 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const uint64_t avail = pool_end - pool_next;
       uint64_t nb = P, ne = P;
       if (avail < n_need) {  // refill: one atomic per BATCH paths
-        // lane 0 takes BATCH ids and hands the base to the wave through LDS (a `b = 0` default
+        // lane 0 takes BATCH ids and hands them to the wave through LDS (a `b = 0` default
         // for the other lanes would be one more loop-carried VGPR pair)
-        if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
-        const uint64_t b = rfl64(pool[2]);
-        if (b < P) {
-          nb = b;
-          ne = b + batch < P ? b + batch : P;
+        if constexpr (SHARD) {
+          uint64_t b, e;
+          refill(b, e);
+          if (b < e) {
+            nb = b;
+            ne = e;
+          } else {
+            exhausted = true;
+          }
         } else {
-          exhausted = true;
+          if (lane == 0) pool[2] = atomicAdd(dispenser, (unsigned long long)batch);
+          const uint64_t b = rfl64(pool[2]);
+          if (b < P) {
+            nb = b;
+            ne = b + batch < P ? b + batch : P;
+          } else {
+            exhausted = true;
+          }
         }
       }
       const uint64_t t_sp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -2093,7 +2140,11 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         // trace_run tripped its guard (a corrupt tree; the frame is invalid and reported): close the path queue
         // for every wave and empty this wave's id pool, so the grid drains after about one trip per wave
         // instead of one per 64 paths (a trip is 2^20 node-loop iterations)
-        atomicMax(dispenser, (unsigned long long)P);
+        if constexpr (SHARD) {
+          for (uint32_t d = 0; d < DISP; ++d) atomicMax(dispenser + d * DISP_STRIDE, (unsigned long long)NB);
+        } else {
+          atomicMax(dispenser, (unsigned long long)P);
+        }
         pool[0] = pool[1];
       }
     } else {
@@ -2443,7 +2494,7 @@ int upload(Scene& s, int device) {
     c.bytes = blob.size();
     HIPCHK(hipMalloc(&c.block, c.bytes), "hipMalloc(scene)");
     HIPCHK(hipMemcpy(c.block, blob.data(), c.bytes, hipMemcpyHostToDevice), "hipMemcpy(scene)");
-    HIPCHK(hipMalloc((void**)&c.counters, 32 * sizeof(unsigned long long)), "hipMalloc(counters)");
+    HIPCHK(hipMalloc((void**)&c.counters, COUNTER_WORDS * sizeof(unsigned long long)), "hipMalloc(counters)");
     // the sticky traversal-error word lives in host memory the kernel writes through (coherent,
     // mapped): the host reads it without a device round trip, also for renders it did not wait for
     HIPCHK(hipHostMalloc((void**)&c.err_host, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc(error word)");
@@ -2728,8 +2779,8 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
   a.seed_hash = z ^ (z >> 31);
   a.out = d_out;
   a.counters = c.counters;
-  a.queue = c.counters + 31;
-  HIPCHK(hipMemsetAsync(c.counters, 0, 32 * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  a.queue = c.counters + 32;  // the DISP path-id dispensers (path_kernel), DISP_STRIDE words apart
+  HIPCHK(hipMemsetAsync(c.counters, 0, COUNTER_WORDS * sizeof(unsigned long long), stream), "hipMemsetAsync");
   if (ev0) HIPCHK(hipEventRecord(ev0, stream), "hipEventRecord");
   if (n_slots && (spp == 0 || max_depth == 0)) {  // lib.rs:83 loops 0 times / :98 returns black
     size_t n = a.packed_out ? (size_t)n_slots * 64 * 3 : (size_t)w * h * 3;
@@ -2799,7 +2850,10 @@ int enqueue_render(Scene& sc, DeviceCopy& c, const rtw_camera* cam, const float 
       a.batch = batch0;
       if (batch_auto)
         while (a.batch / 2u >= batch_floor && a.n_paths < (uint64_t)a.batch * waves * 32u) a.batch /= 2u;
-      if (base) HIPCHK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), stream), "hipMemsetAsync(queue)");
+      // (a pass the rule above gave smaller batches spreads its atomics over DISP words in the LDS-node kernels:
+      // path_kernel SHARD; r06 share8: an 8-GPU share of jumpy-1080p +5%, configs[0] +11%)
+      if (base) HIPCHK(hipMemsetAsync(a.queue, 0, DISP * DISP_STRIDE * sizeof(unsigned long long), stream),
+                       "hipMemsetAsync(queue)");
       hipEvent_t* ke = reinterpret_cast<hipEvent_t*>(c.kev[c.kev_head]);
       if (!ke[0]) HIPCHK(hipEventCreate(&ke[0]), "hipEventCreate");
       if (!ke[1]) HIPCHK(hipEventCreate(&ke[1]), "hipEventCreate");

@@ -97,7 +97,7 @@ struct DeviceCopy {
   void* block = nullptr;  // one hipMalloc holding every table
   size_t bytes = 0;
   DevScene scene{};
-  unsigned long long* counters = nullptr;  // 32 x u64: [0..23] stats, [31] path queue
+  unsigned long long* counters = nullptr;  // COUNTER_WORDS x u64: [0..31] stats, then the path-id dispensers
   // host-mapped sticky error word (hipHostMalloc): a path kernel whose traversal guard trips writes 1;
   // the host reads it at the next render call, rtw_render_status, rtw_path_kernel_times and with stats
   uint32_t* err_host = nullptr;
