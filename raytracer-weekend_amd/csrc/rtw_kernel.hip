@@ -17,7 +17,7 @@
 // conservative (padded boxes + slack), so it changes which nodes are visited, never the answer.
 //
 // Kernel structure: path_kernel is PERSISTENT -- the grid is the resident capacity,
-// and each wave draws path ids from one global queue (RenderArgs::batch per atomic: 1024 in the
+// and each wave draws path ids from a global queue (RenderArgs::batch per atomic: 1024 in the
 // 1024-lane LDS-node and the list-mode kernels, 2048 elsewhere; knob RTW_BATCH) into an LDS pool, hands
 // them to its idle lanes by ballot + mbcnt prefix (64 consecutive ids = one sample of one 8x8 tile), and
 // loops: regenerate -> trace_begin (the always-tested list) -> trace_run (resumable BVH4 walk with
@@ -1745,8 +1745,8 @@ __device__ __forceinline__ float reflectance(float cosine, float r0) {  // mater
 // grid drains with a one-path tail.  Each finished path writes L to the ordered sample
 // buffer (path-major RGB, 12 B per path in HBM); reduce_kernel then sums each pixel's samples in
 // sample order — exactly lib.rs:83-87's `pixel_color += sample_ray(..)` sequence.
-// Path ids a wave takes per returning atomic on the one global queue word.  Every wave of the
-// grid hits that word: at 256 ids per atomic, short-path scenes spent most of their time behind it
+// Path ids a wave takes per returning atomic on the global queue word (path_kernel SHARD: eight).  Every wave of
+// the grid hits that word: at 256 ids per atomic, short-path scenes spent most of their time behind it
 // (MI355X, RTW_BATCH sweep: cow-1080p 19.0k -> 30.1k Mrays/s, monument-4k 12.8k -> 17.0k, jumpy-1080p
 // 19.4k -> 20.4k at 2048); the tail this leaves is one batch per wave (~0.1 ms).  Knob RTW_BATCH.
 constexpr uint32_t BATCH = 2048;
